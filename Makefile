@@ -1,0 +1,48 @@
+# In-tree build: the .so files travel to the GPU box with the gpurun snapshot.
+#   build/librtmi355x.so   HIP kernels + C ABI (include/rt_mi355x.h)   <- the product
+#   build/librthost.so     C++ scene builder + output stage (include/rt_host.h)
+#   build/rt_render_cli    main.rs-equivalent host program (preset -> PPM)
+#   oracle/_build/*.so     CPU restatement (test infrastructure only)
+PKG      := surely-raytracing_amd
+CSRC     := $(PKG)/csrc
+BUILD    := build
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+# device path is f64; contraction off, fma written explicitly (deterministic bits)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra
+CFLAGS_O := -std=c11 -O2 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+
+HOST_SRC := $(CSRC)/host/scene.cpp $(CSRC)/host/presets.cpp $(CSRC)/host/capi.cpp
+DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp
+DEV_HDR  := $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp include/rt_mi355x.h
+
+.PHONY: all device host oracle cli clean
+all: device host oracle cli
+
+device: $(BUILD)/librtmi355x.so
+host: $(BUILD)/librthost.so
+cli: $(BUILD)/rt_render_cli
+oracle: oracle/_build/liboracle_f32.so oracle/_build/liboracle_f64.so
+
+$(BUILD)/librtmi355x.so: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -shared $(DEV_SRC) -o $@
+
+$(BUILD)/librthost.so: $(HOST_SRC) $(CSRC)/host/scene.hpp include/rt_host.h include/rt_mi355x.h
+	@mkdir -p $(BUILD)
+	g++ $(CXXFLAGS) -shared $(HOST_SRC) -o $@
+
+$(BUILD)/rt_render_cli: $(CSRC)/host/rt_render_cli.cpp $(BUILD)/librthost.so $(BUILD)/librtmi355x.so
+	g++ $(CXXFLAGS) $< -o $@ -L$(BUILD) -lrthost -lrtmi355x -Wl,-rpath,'$$ORIGIN'
+
+oracle/_build/liboracle_f32.so: oracle/rt_oracle.c include/rt_mi355x.h
+	@mkdir -p oracle/_build
+	gcc $(CFLAGS_O) -DORACLE_F64=0 -shared $< -o $@ -lpthread -lm
+
+oracle/_build/liboracle_f64.so: oracle/rt_oracle.c include/rt_mi355x.h
+	@mkdir -p oracle/_build
+	gcc $(CFLAGS_O) -DORACLE_F64=1 -shared $< -o $@ -lpthread -lm
+
+clean:
+	rm -rf $(BUILD) oracle/_build

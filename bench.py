@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the per-pixel render loop on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[1]): the reference's cornell_box scene
+(main.rs:417-512) with mixture-PDF light sampling, 800x800, 1000 spp -> 961 effective
+(nearest_square, render.rs:38-41), max depth 50, render seed 1.
+
+A "step" = one full frame: every rank renders its cyclic share of the 800 rows
+(row r -> rank r % N, no data-path collective) into a device buffer, then the frame is
+gathered to rank 0 (torch.distributed: RCCL over xGMI). Scene upload, RCCL init and the
+op-count pass are outside the timed region. value = W*H*spp_eff*steps / max-over-ranks time.
+
+Also reported (one JSON line on rank 0):
+  roofline     FP64 VALU roofline of rt_trace: counted algorithmic flops per launch / the
+               kernel's average duration (torch.cuda.Event on the launch stream), vs 78.6 TF.
+  scene_fetch  the north star's "HBM GB/s on BVH traversal": logical scene-record bytes / time.
+  cpu_baseline the f64 CPU oracle (a restatement of the reference; the Rust original cannot be
+               built here) on this host's cores, timed on a bounded stratum subset of the same
+               frame (rank 0, N = 1 only).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--width 800] [--spp 1000]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "surely-raytracing_amd"))
+
+METRIC = "Msamples/sec (pixels*spp/s), Cornell box 800x800 @ 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell_box")
+    ap.add_argument("--width", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU-baseline work (bounded sample)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-count", action="store_true", help="skip the op-count pass")
+    return ap.parse_args()
+
+
+def cpu_baseline(blob, cam, seed, target_s):
+    """f64 CPU oracle on a bounded sample of the same frame: full image, a subset of the
+    sqrt_spp stratum rows (each sample keeps the full-spp jitter), 3-row chunks over a thread
+    pool (render.rs:171)."""
+    sys.path.insert(0, str(REPO / "tests"))
+    import oracle_lib as O
+    import surely_rt as rt
+
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(16, threads))
+    done_samples, elapsed, sj = 0, 0.0, 0
+    S = cam.sqrt_spp
+    while sj < S and elapsed < target_s:
+        opts = rt.make_opts(cam, seed=seed, sj_begin=(S // 2 + sj) % S, sj_count=1)
+        t0 = time.perf_counter()
+        O.render(blob, cam, opts, precision=64, threads=threads)
+        elapsed += time.perf_counter() - t0
+        done_samples += cam.image_width * cam.image_height * S
+        sj += 1
+    return {
+        "value": done_samples / elapsed / 1e6,
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{sj} of {S} stratum rows (s_j) over the full {cam.image_width}x"
+                   f"{cam.image_height} frame = {done_samples} samples in {elapsed:.1f} s; "
+                   "f64 C restatement of the reference (oracle/rt_oracle.c), 3-row chunks"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import surely_rt as rt
+    from surely_rt import roofline
+    from surely_rt.parallel import cyclic_rows, gather_frame, max_rows
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    blob, cam = rt.preset_blob(args.scene, width=args.width, spp=args.spp, depth=args.depth)
+    W, H, spp = cam.image_width, cam.image_height, cam.samples_per_pixel
+    ds = rt.DeviceScene(blob, device=local)
+    b, s, n = cyclic_rows(H, rank, world)
+    m = max_rows(H, world)
+    local_buf = torch.zeros((m, W, 3), dtype=torch.float32, device=f"cuda:{local}")
+    opts = rt.make_opts(cam, seed=args.seed, row_begin=b, row_step=s, n_rows=n,
+                        flags=rt.RT_FLAG_OVERWRITE, device=local)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        return gather_frame(local_buf, H, rank, world)
+
+    # ---- op counts for the roofline (outside the timed region; deterministic)
+    ops = None
+    if not args.no_count:
+        copts = rt.make_opts(cam, seed=args.seed, row_begin=b, row_step=s, n_rows=n,
+                             flags=rt.RT_FLAG_OVERWRITE | rt.RT_FLAG_COUNT_OPS, device=local)
+        st = ds.render_device(cam, copts, local_buf.data_ptr(), stream.cuda_stream, stats=True)
+        ops = st.op_counts()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    frame = None
+    for k in range(args.steps):
+        frame = step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(1, args.steps)
+
+    if rank == 0:
+        total = W * H * spp * args.steps
+        value = total / elapsed / 1e6
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (procedural reference scene, no input data)",
+            "config": {
+                "workload": f"{args.scene} {W}x{H}, {args.spp}->{spp} spp, depth {cam.max_depth}"
+                            " (BASELINE configs[1])",
+                "width": W, "height": H, "spp_effective": spp, "max_depth": cam.max_depth,
+                "seed": args.seed, "parallelism": f"cyclic rows x{world}, gather to rank 0",
+            },
+        }
+        if ops is not None:
+            # flops / bytes of the rank-0 launch (its share of rows) over its kernel time
+            fl = roofline.flops(ops)
+            by = roofline.scene_bytes(ops, partial_bytes=n * W * 12 * cam.sqrt_spp)
+            ach = fl / (kernel_ms * 1e-3) / 1e12
+            traffic = None
+            tf = REPO / "profiles" / "pmc_traffic.json"
+            if tf.exists():
+                try:
+                    traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            res["roofline"] = {
+                "bound": "valu", "achieved": round(ach, 3),
+                "peak": roofline.PEAK_FP64_VECTOR_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / roofline.PEAK_FP64_VECTOR_TFLOPS, 4),
+                "traffic": traffic,
+                "kernel": "rt_trace", "kernel_ms": round(kernel_ms, 3),
+                "flops_per_launch": fl, "flops_per_sample": round(fl / ops["samples"], 1),
+            }
+            gbps = by / (kernel_ms * 1e-3) / 1e9
+            res["scene_fetch"] = {
+                "achieved": round(gbps, 1), "peak": roofline.PEAK_HBM_GBPS, "unit": "GB/s",
+                "frac": round(gbps / roofline.PEAK_HBM_GBPS, 4),
+                "bytes_per_launch": by,
+                "note": "logical scene-record bytes (L1/L2-resident), not HBM traffic",
+            }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(blob, cam, args.seed, args.cpu_seconds)
+            res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
+        assert frame is not None and frame.shape == (H, W, 3)
+        print(json.dumps(res), flush=True)
+    ds.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

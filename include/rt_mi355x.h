@@ -1,0 +1,219 @@
+/*
+ * rt_mi355x.h — C ABI of the MI355X (gfx950) path-tracing library `librtmi355x.so`.
+ *
+ * This is the drop-in boundary for the reference's per-pixel render loop:
+ *
+ *   reference (Rust, no FFI exists upstream)           this ABI
+ *   -----------------------------------------------    ------------------------------------------
+ *   render_par_lights(cam, world, pixels, suns, lights) rt_render / rt_render_device
+ *       /root/reference/src/render.rs:144-216               (scene blob + camera + opts -> accum)
+ *   render_par(cam, world, pixels, suns)                rt_render with blob.lights_off == -1
+ *       /root/reference/src/render.rs:140-142               (empty light list, see RT_FLAG_SEMANTICS_REFERENCE)
+ *   Camera::new derived fields                          rt_camera (filled host-side, render.rs:62-133)
+ *       /root/reference/src/render.rs:15-36
+ *   HittableList / Object tree (world, lights)          rt_scene_blob (prefix-serialised tree,
+ *       /root/reference/src/hittable.rs:55-130,             f64 slots, see "Scene blob" below)
+ *       object.rs:17-71, transform.rs, constant_medium.rs
+ *   pixels: &mut Vec<Color> (raw sums, pre-zeroed)      float* accum_rgb (raw sums over spp,
+ *       /root/reference/src/render.rs:136-138, 189          added into unless RT_FLAG_OVERWRITE)
+ *   panics (expect / panic!)                            int status < 0 + rt_last_error()
+ *
+ * Output stays host-side: write_color / the PPM writer (color.rs:8-33) are NOT behind this ABI;
+ * accum holds raw per-pixel sums exactly like the reference's `pixels` vector.
+ *
+ * Every entry point is plain C: pointers, sizes, PODs. No torch, no C++ types.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------------ */
+#define RT_OK 0
+#define RT_ERR_INVALID_ARG (-1)
+#define RT_ERR_BAD_BLOB (-2)      /* malformed scene blob                                   */
+#define RT_ERR_UNSUPPORTED (-3)   /* valid reference scene the device path cannot express    */
+#define RT_ERR_EMPTY_LIGHTS (-4)  /* reference semantics: empty light list panics            */
+                                  /* (hittable.rs:115-129 via render.rs:140-142)            */
+#define RT_ERR_HIP (-5)           /* HIP runtime failure (message in rt_last_error)         */
+#define RT_ERR_NO_DEVICE (-6)
+
+/* ---- scene blob ---------------------------------------------------------------------------
+ * A flat array of 64-bit slots. A slot holds an int64 or the bit pattern of an IEEE f64.
+ * The host computes every derived quantity in f64 exactly as the reference constructors do
+ * (Quad::new object.rs:427-446, Sphere::new 83-105, RotateY::new transform.rs:143-186, ...);
+ * consumers round to their working precision.
+ *
+ * Header (slot index: meaning)
+ *   0 magic RT_BLOB_MAGIC      1 version RT_BLOB_VERSION    2 n_slots
+ *   3 n_textures  4 textures_off   (RT_TEX_SLOTS slots each)
+ *   5 n_materials 6 materials_off  (RT_MAT_SLOTS slots each)
+ *   7 n_perlin    8 perlin_off     (RT_PERLIN_SLOTS each: ranvec 256x3 f64, perm_x/y/z 3x256 int)
+ *   9 world_off                    (object tree: the world HittableList)
+ *  10 lights_off                   (object tree, or -1 = empty light list, as render_par)
+ *  11 n_texel_bytes                (size of blob.texels; images index into it)
+ *
+ * Object tree: prefix order, records by tag (slot counts include the tag):
+ *   RT_OBJ_LIST      [tag, n, bbox6]                       then n children      (hittable.rs:55-130)
+ *   RT_OBJ_BVH       [tag, bbox6]                          then left, right     (hittable.rs:135-241)
+ *   RT_OBJ_SPHERE    [tag, mat, moving, c3, radius, cvec3, bbox6]               (object.rs:73-213)
+ *   RT_OBJ_QUAD      [tag, mat, q3, u3, v3, normal3, w3, d, area, bbox6]        (object.rs:414-507)
+ *   RT_OBJ_TRANSLATE [tag, offset3, bbox6]                 then child           (transform.rs:19-74)
+ *   RT_OBJ_ROTATE_Y  [tag, sin, cos, bbox6]                then child           (transform.rs:76-186)
+ *   RT_OBJ_VOLUME    [tag, mat, neg_inv_density, bbox6]    then boundary        (constant_medium.rs)
+ *   bbox6 = xmin xmax ymin ymax zmin zmax.
+ * Material record [kind, p0..p6]:
+ *   LAMBERTIAN [1, tex]   METAL [2, r, g, b, fuzz]   DIELECTRIC [3, ir, r, g, b]
+ *   DIFFUSE_LIGHT [4, tex]   ISOTROPIC [5, tex]                                 (material.rs:25-248)
+ * Texture record [kind, p0..p6]:
+ *   SOLID [1, r, g, b]   CHECKER [2, inv_scale, even_tex, odd_tex]
+ *   IMAGE [3, width, height, texel_byte_offset]  (width or height 0 = image absent -> (0,1,1))
+ *   NOISE [4, scale, perlin_index]                                              (texture.rs:10-131)
+ * ------------------------------------------------------------------------------------------ */
+#define RT_BLOB_MAGIC 0x52545343 /* 'RTSC' */
+#define RT_BLOB_VERSION 1
+#define RT_BLOB_HEADER_SLOTS 16
+#define RT_TEX_SLOTS 8
+#define RT_MAT_SLOTS 8
+#define RT_PERLIN_POINTS 256
+#define RT_PERLIN_SLOTS (RT_PERLIN_POINTS * 3 + RT_PERLIN_POINTS * 3)
+
+enum rt_obj_tag {
+  RT_OBJ_LIST = 1,
+  RT_OBJ_BVH = 2,
+  RT_OBJ_SPHERE = 3,
+  RT_OBJ_QUAD = 4,
+  RT_OBJ_TRANSLATE = 5,
+  RT_OBJ_ROTATE_Y = 6,
+  RT_OBJ_VOLUME = 7
+};
+enum rt_mat_kind {
+  RT_MAT_LAMBERTIAN = 1,
+  RT_MAT_METAL = 2,
+  RT_MAT_DIELECTRIC = 3,
+  RT_MAT_DIFFUSE_LIGHT = 4,
+  RT_MAT_ISOTROPIC = 5
+};
+enum rt_tex_kind { RT_TEX_SOLID = 1, RT_TEX_CHECKER = 2, RT_TEX_IMAGE = 3, RT_TEX_NOISE = 4 };
+
+typedef struct rt_scene_blob {
+  const uint64_t* slots;
+  uint64_t n_slots;
+  const uint8_t* texels; /* RGB8 images, row-major, top row first (as image::to_rgb8) */
+  uint64_t n_texels;
+} rt_scene_blob;
+
+/* ---- camera: Camera's derived fields (render.rs:15-36), computed on the host in f64 ---------- */
+typedef struct rt_camera {
+  int32_t image_width;
+  int32_t image_height;
+  int32_t samples_per_pixel; /* effective spp = nearest_square(spp) (render.rs:38-41, 108) */
+  int32_t sqrt_spp;
+  int32_t max_depth;
+  int32_t _pad0;
+  double recip_sqrt_spp;
+  double center[3];
+  double pixel00_loc[3];
+  double pixel_delta_u[3];
+  double pixel_delta_v[3];
+  double defocus_angle;
+  double defocus_disk_u[3];
+  double defocus_disk_v[3];
+  double background[3];
+} rt_camera;
+
+/* ---- render options ---------------------------------------------------------------------- */
+#define RT_FLAG_OVERWRITE 0x1u             /* accum = sums instead of accum += sums          */
+#define RT_FLAG_COUNT_OPS 0x2u             /* run the op-counting build, fill rt_stats.ops   */
+#define RT_FLAG_SEMANTICS_REFERENCE 0x4u   /* exact reference semantics: empty lights -> error, */
+                                           /* Isotropic scattering_pdf = 0 */
+
+typedef struct rt_render_opts {
+  uint64_t seed;      /* render RNG seed                                   */
+  int32_t row_begin;  /* first image row of this call                                          */
+  int32_t row_step;   /* 1 = contiguous band; G = cyclic tiling (rows row_begin + k*G)         */
+  int32_t n_rows;     /* rows rendered; accum holds n_rows * image_width * 3 floats            */
+  uint32_t flags;     /* RT_FLAG_*                                                             */
+  int32_t sj_begin;   /* stratum rows [sj_begin, sj_begin+sj_count) of the sqrt_spp x sqrt_spp */
+  int32_t sj_count;   /* grid (render.rs:185); 0 = all. A subset keeps the full-spp jitter.   */
+  int32_t device;     /* HIP device ordinal (rt_render only)                                   */
+  int32_t _pad0;
+} rt_render_opts;
+
+/* Deterministic op counters (RT_FLAG_COUNT_OPS). Identical paths => identical counts on the
+ * CPU oracle and the GPU, so per-sample work is measured, not assumed. */
+enum rt_op_counter {
+  RT_OP_SAMPLES = 0,      /* camera paths started                                     */
+  RT_OP_WORLD_QUERIES,    /* world.hit calls (render.rs:264)                          */
+  RT_OP_QUAD_TESTS,       /* Quad::hit entered (object.rs:453)                        */
+  RT_OP_QUAD_PLANE,       /* ... passed the |n.d| >= 1e-8 test                        */
+  RT_OP_QUAD_INTERVAL,    /* ... t inside the interval: planar coords computed        */
+  RT_OP_QUAD_HITS,        /* ... accepted                                             */
+  RT_OP_SPHERE_TESTS,     /* Sphere::hit entered (object.rs:145)                      */
+  RT_OP_SPHERE_ROOTS,     /* ... discriminant >= 0                                    */
+  RT_OP_SPHERE_HITS,      /* ... accepted                                             */
+  RT_OP_AABB_TESTS,       /* Aabb::hit (object.rs:340) from BvhNode::hit              */
+  RT_OP_TRANSLATE,        /* Translate::hit entered                                   */
+  RT_OP_ROTATE_Y,         /* RotateY::hit entered                                     */
+  RT_OP_VOLUME_TESTS,     /* ConstantMedium::hit entered                              */
+  RT_OP_VOLUME_DRAWS,     /* ... free-flight distance drawn                           */
+  RT_OP_MISSES,           /* world miss -> background                                 */
+  RT_OP_EMISSIVE_HITS,    /* DiffuseLight hit (path ends)                             */
+  RT_OP_LAMBERTIAN,       /* Lambertian scatter + mixture PDF                         */
+  RT_OP_METAL,
+  RT_OP_DIELECTRIC,
+  RT_OP_ISOTROPIC,
+  RT_OP_LIGHT_PDF_QUAD,   /* Quad::pdf_value (object.rs:492)                          */
+  RT_OP_LIGHT_PDF_SPHERE, /* Sphere::pdf_value (object.rs:190)                        */
+  RT_OP_LIGHT_GEN,        /* light-PDF generate (pdf.rs:120-126, first branch)        */
+  RT_OP_COSINE_GEN,       /* material-PDF generate                                    */
+  RT_OP_NOISE_EVALS,      /* NoiseTexture::value (texture.rs:127-130)                 */
+  RT_OP_DEPTH_CUTOFF,     /* path ended by max_depth                                  */
+  RT_OP_COUNT
+};
+
+typedef struct rt_stats {
+  double ms_kernel;  /* device time of the render kernels (HIP events)             */
+  double ms_total;   /* host wall time of the call                                  */
+  uint64_t samples;  /* pixel-samples rendered by this call                         */
+  uint64_t ops[32];  /* rt_op_counter values (RT_FLAG_COUNT_OPS only)               */
+} rt_stats;
+
+typedef struct rt_scene rt_scene; /* opaque: device-resident flattened scene + workspace */
+
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+
+/* Validate a blob without touching a device (hittable/object invariants, tag and index ranges). */
+int rt_scene_validate(const rt_scene_blob* blob);
+
+/* Validate, flatten (threaded node array, f32) and upload to `device`. */
+int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+/* Bytes of the device-side flattened scene (nodes + materials + textures + tables). */
+uint64_t rt_scene_device_bytes(const rt_scene* scene);
+
+/* Synchronous: render into a HOST buffer (n_rows * W * 3 floats). */
+int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts, float* accum_rgb,
+              rt_stats* stats);
+
+/* Asynchronous on `hip_stream` (hipStream_t, may be NULL): render into a DEVICE buffer.
+ * If stats != NULL the call synchronises the stream to fill it. */
+int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
+                     float* accum_rgb_device, void* hip_stream, rt_stats* stats);
+
+/* One-shot drop-in for render_par_lights: create + render + destroy. */
+int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
+                   float* accum_rgb, rt_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

@@ -1,0 +1,1065 @@
+// rt_device.hip — gfx950 path-tracing kernels + the C ABI of include/rt_mi355x.h.
+//
+// Replaces the reference's per-pixel render loop (render.rs:144-216) and everything it calls:
+// get_ray (render.rs:218-249), ray_color (render.rs:251-311), HittableList/BvhNode::hit
+// (hittable.rs:88-109, 216-236), Quad/Sphere/Aabb::hit (object.rs:145-184, 340-370, 453-490),
+// Translate/RotateY::hit (transform.rs:57-135), ConstantMedium::hit (constant_medium.rs:41-95),
+// Material scatter (material.rs:92-248), PDFs (pdf.rs:44-127), Onb (onb.rs:24-47), textures
+// and Perlin noise (texture.rs:17-131, perlin.rs:30-96), vec3 math (vec3.rs).
+//
+// Work decomposition: one lane = one (pixel, stratum row s_j); the lane walks
+// the sqrt_spp samples s_i of that row, regenerating a camera path as soon as the previous one
+// terminates (ray_color's recursion -> an iterative bounce loop with beta/L), so lanes of a
+// wave stay busy while path lengths differ. A wave = an 8x8 pixel tile at one s_j; the tile's
+// rows are adjacent, so camera rays and first hits are coherent. Row sums go to a per-(s_j,
+// pixel) partial buffer; rt_reduce sums them in s_j order into the caller's accumulator.
+// No atomics touch the framebuffer: the sum order is fixed, so results are bitwise
+// reproducible and identical across 1..8 GPUs (the RNG is keyed by global pixel and sample).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_flatten.hpp"
+#include "rt_layout.h"
+#include "rt_rng.h"
+
+using namespace rtd;
+
+namespace {
+
+// The path is computed in f64 like the reference (vec3.rs:21-25 f64 everywhere): its fixed
+// epsilons (t_min 1e-4 render.rs:267, 1e-3 light PDFs object.rs:193,493, 1e-8 quad
+// parallelism object.rs:457) assume f64 hit points; at fp32 the glass sphere and the ground
+// boxes self-intersect. MI355X runs FP64 FMA at half its FP32 rate.
+constexpr double kPi = 3.14159265358979323846;
+constexpr int kWaveTile = 8;  // 8x8 pixels per wave
+constexpr int kBlock = 256;   // 4 waves per workgroup
+
+struct d3 {
+  double x, y, z;
+};
+__device__ __forceinline__ d3 mk(double x, double y, double z) { return {x, y, z}; }
+__device__ __forceinline__ d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ d3 operator-(d3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ d3 operator*(d3 a, d3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ d3 operator*(d3 a, double t) { return {a.x * t, a.y * t, a.z * t}; }
+__device__ __forceinline__ d3 operator*(double t, d3 a) { return {a.x * t, a.y * t, a.z * t}; }
+// Contraction is OFF for the device build (-ffp-contract=off): every fma below is explicit, so
+// an expression computes the same bits in every inlining context. The reference relies on
+// that determinism: a sphere that is both a world object and a ConstantMedium boundary
+// (main.rs:656-666) must yield the identical t from both tests, or constant_medium.rs:52-55
+// draws an extra random number.
+__device__ __forceinline__ double dot(d3 u, d3 v) {  // vec3.rs:167
+  return fma(u.x, v.x, fma(u.y, v.y, u.z * v.z));
+}
+__device__ __forceinline__ d3 vfma(double t, d3 a, d3 b) {  // t*a + b
+  return {fma(t, a.x, b.x), fma(t, a.y, b.y), fma(t, a.z, b.z)};
+}
+__device__ __forceinline__ d3 cross(d3 u, d3 v) {  // vec3.rs:171-177
+  return {fma(u.y, v.z, -(u.z * v.y)), fma(u.z, v.x, -(u.x * v.z)), fma(u.x, v.y, -(u.y * v.x))};
+}
+__device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
+  double inv = 1.0 / sqrt(dot(v, v));
+  return v * inv;
+}
+__device__ __forceinline__ d3 reflect(d3 v, d3 n) {  // vec3.rs:219-221
+  return vfma(-2.0 * dot(v, n), n, v);
+}
+__device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-229
+  double c = fmin(dot(-uv, n), 1.0);
+  d3 perp = e * vfma(c, n, uv);
+  return vfma(-sqrt(fabs(1.0 - dot(perp, perp))), n, perp);
+}
+
+// sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (vec3.rs:244, object.rs:127: phi = 2*pi*r1).
+// Exact reduction to a quarter-turn fraction r in [-1/2, 1/2], then Taylor series of
+// theta = r*pi/2 (|theta| <= pi/4) to theta^19 / theta^18: < 1 ulp, and none of the large-
+// argument machinery of the general sincos (which cost ~40 VGPRs here).
+__device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
+  double t = 4.0 * u;
+  double k = floor(t + 0.5);
+  double th = (t - k) * (0.5 * kPi);
+  double x2 = th * th;
+  double s = 1.0 / 121645100408832000.0;  // 1/19!
+  s = s * -x2 + 1.0 / 355687428096000.0;
+  s = s * -x2 + 1.0 / 1307674368000.0;
+  s = s * -x2 + 1.0 / 6227020800.0;
+  s = s * -x2 + 1.0 / 39916800.0;
+  s = s * -x2 + 1.0 / 362880.0;
+  s = s * -x2 + 1.0 / 5040.0;
+  s = s * -x2 + 1.0 / 120.0;
+  s = s * -x2 + 1.0 / 6.0;
+  s = (s * -x2 + 1.0) * th;
+  double c = 1.0 / 6402373705728000.0;  // 1/18!
+  c = c * -x2 + 1.0 / 20922789888000.0;
+  c = c * -x2 + 1.0 / 87178291200.0;
+  c = c * -x2 + 1.0 / 479001600.0;
+  c = c * -x2 + 1.0 / 3628800.0;
+  c = c * -x2 + 1.0 / 40320.0;
+  c = c * -x2 + 1.0 / 720.0;
+  c = c * -x2 + 1.0 / 24.0;
+  c = c * -x2 + 0.5;
+  c = c * -x2 + 1.0;
+  int q = ((int)k) & 3;
+  *so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
+  *co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
+}
+
+struct TraceParams {
+  const uint32_t* __restrict__ nodes;
+  const uint32_t* __restrict__ mats;
+  const uint32_t* __restrict__ texs;
+  const uint8_t* __restrict__ perlin;
+  const uint32_t* __restrict__ lights;
+  const uint32_t* __restrict__ light_offs;
+  const uint8_t* __restrict__ texels;
+  float* __restrict__ partial;
+  unsigned long long* __restrict__ ops;
+  uint32_t root, n_lights, lights_is_list, flags;
+  double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
+  double rs;
+  int defocus;
+  int W, n_rows, row_begin, row_step, sqrt_spp, sj0, n_sj, max_depth;
+  uint32_t seed_lo, seed_hi;
+  int tiles_x;
+};
+
+// ---------------------------------------------------------------- loads (16 B, dwordx4)
+__device__ __forceinline__ double2 ldd2(const uint32_t* p) {
+  return *reinterpret_cast<const double2*>(p);
+}
+// xyz of the f64 triple starting at double index k of a node (payload begins at word 4)
+__device__ __forceinline__ d3 ld3(const uint32_t* X, int k) {
+  const double* d = reinterpret_cast<const double*>(X + 4) + k;
+  double2 a = *reinterpret_cast<const double2*>(d);
+  return mk(a.x, a.y, d[2]);
+}
+__device__ __forceinline__ double ldd(const uint32_t* X, int k) {
+  return reinterpret_cast<const double*>(X + 4)[k];
+}
+__device__ __forceinline__ uint4 ld4u(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ d3 arr3(const double* a) { return mk(a[0], a[1], a[2]); }
+
+// ---------------------------------------------------------------- op counters (COUNT build)
+template <bool COUNT>
+struct Ctr {
+  __device__ __forceinline__ void inc(int) {}
+  __device__ __forceinline__ void flush(unsigned int*) {}
+};
+template <>
+struct Ctr<true> {
+  uint32_t c[RT_OP_COUNT];
+  __device__ Ctr() {
+#pragma unroll
+    for (int k = 0; k < RT_OP_COUNT; ++k) c[k] = 0;
+  }
+  __device__ __forceinline__ void inc(int k) { c[k]++; }
+  __device__ void flush(unsigned int* sh) {
+#pragma unroll
+    for (int k = 0; k < RT_OP_COUNT; ++k)
+      if (c[k]) atomicAdd(&sh[k], c[k]);
+  }
+};
+
+// ---------------------------------------------------------------- primitives
+// Quad::hit object.rs:453-490; inclusive interval (Interval::contains interval.rs:21-23).
+template <bool COUNT>
+__device__ __forceinline__ bool quad_test(const uint32_t* q, d3 o, d3 d, double tmin, double tmax,
+                                          double& t_out, Ctr<COUNT>& C) {
+  C.inc(RT_OP_QUAD_TESTS);
+  double2 n01 = ldd2(q + 4), n2D = ldd2(q + 8);
+  d3 n = mk(n01.x, n01.y, n2D.x);
+  double denom = dot(n, d);
+  if (fabs(denom) < 1e-8) return false;
+  C.inc(RT_OP_QUAD_PLANE);
+  double t = (n2D.y - dot(n, o)) / denom;
+  if (!(tmin <= t && t <= tmax)) return false;
+  C.inc(RT_OP_QUAD_INTERVAL);
+  d3 p = vfma(t, d, o);
+  d3 pq = p - ld3(q, 4);
+  d3 w = ld3(q, 8);
+  double a = dot(w, cross(pq, ld3(q, 16)));
+  double b = dot(w, cross(ld3(q, 12), pq));
+  if (a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b) return false;
+  C.inc(RT_OP_QUAD_HITS);
+  t_out = t;
+  return true;
+}
+
+// Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
+template <bool COUNT>
+__device__ __forceinline__ bool sphere_test(const uint32_t* s, d3 o, d3 d, double tm, double tmin,
+                                            double tmax, double& t_out, Ctr<COUNT>& C) {
+  C.inc(RT_OP_SPHERE_TESTS);
+  double2 c01 = ldd2(s + 4), c2r = ldd2(s + 8);
+  d3 center = mk(c01.x, c01.y, c2r.x);
+  if (s[3]) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
+  d3 oc = o - center;
+  double a = dot(d, d);
+  double half_b = dot(oc, d);
+  double c = dot(oc, oc) - c2r.y * c2r.y;
+  double disc = fma(half_b, half_b, -(a * c));
+  if (disc < 0.0) return false;
+  C.inc(RT_OP_SPHERE_ROOTS);
+  double sqrtd = sqrt(disc);
+  double root = (-half_b - sqrtd) / a;
+  if (!(tmin < root && root < tmax)) {
+    root = (sqrtd - half_b) / a;
+    if (!(tmin < root && root < tmax)) return false;
+  }
+  C.inc(RT_OP_SPHERE_HITS);
+  t_out = root;
+  return true;
+}
+
+// Aabb::hit object.rs:340-370 with inv_d = 1/d computed once per ray frame.
+__device__ __forceinline__ bool aabb_test(const uint32_t* b, d3 o, d3 inv, double tmin,
+                                          double tmax) {
+  double2 bx = ldd2(b + 4), by = ldd2(b + 8), bz = ldd2(b + 12);
+  const double mn[3] = {bx.x, by.x, bz.x}, mx[3] = {bx.y, by.y, bz.y};
+  const double oo[3] = {o.x, o.y, o.z}, id[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    double t0 = (mn[a] - oo[a]) * id[a];
+    double t1 = (mx[a] - oo[a]) * id[a];
+    if (id[a] < 0.0) {
+      double tt = t0;
+      t0 = t1;
+      t1 = tt;
+    }
+    if (t0 > tmin) tmin = t0;
+    if (t1 < tmax) tmax = t1;
+    if (tmax <= tmin) return false;
+  }
+  return true;
+}
+
+// Translate/RotateY ray into object space (transform.rs:59, 86-107).
+__device__ __forceinline__ void xform_in(const uint32_t* X, d3& o, d3& d) {
+  double2 p01 = ldd2(X + 8);
+  if ((X[0] & 0xffu) == RTL_TRANSLATE) {
+    o = o - mk(p01.x, p01.y, ldd(X, 4));
+  } else {
+    double s = p01.x, c = p01.y;
+    o = mk(fma(c, o.x, -(s * o.z)), o.y, fma(s, o.x, c * o.z));
+    d = mk(fma(c, d.x, -(s * d.z)), d.y, fma(s, d.x, c * d.z));
+  }
+}
+// Hit record back to the parent space (transform.rs:65, 114-130).
+__device__ __forceinline__ void xform_out(const uint32_t* X, d3& p, d3& n) {
+  double2 p01 = ldd2(X + 8);
+  if ((X[0] & 0xffu) == RTL_TRANSLATE) {
+    p = p + mk(p01.x, p01.y, ldd(X, 4));
+  } else {
+    double s = p01.x, c = p01.y;
+    p = mk(fma(c, p.x, s * p.z), p.y, fma(-s, p.x, c * p.z));
+    n = mk(fma(c, n.x, s * n.z), n.y, fma(-s, n.x, c * n.z));
+  }
+}
+// Local ray of `frame` = the world ray pushed through its transform chain, root first.
+__device__ __forceinline__ void frame_ray(const uint32_t* __restrict__ N, int frame, d3 wo, d3 wd,
+                                          d3& o, d3& d) {
+  o = wo;
+  d = wd;
+  if (frame < 0) return;
+  uint4 h = ld4u(N + frame);
+  uint4 ch = ld4u(N + frame + 4);
+  const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+  for (int k = 0; k < RTL_MAX_CHAIN; ++k)
+    if ((uint32_t)k < h.z) xform_in(N + c4[k], o, d);
+}
+
+// ---------------------------------------------------------------- traversal
+// Threaded walk of the flattened scene (rt_layout.h). MAIN: the world (records the hit node and
+// its frame, handles ConstantMedium when VOL). !MAIN: a volume boundary (closest t only).
+template <bool MAIN, bool COUNT, bool VOL>
+__device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, double tm, d3 o, d3 d,
+                         int frame, double tmin, double tmax, double& t_out, uint32_t& hit_node,
+                         int& hit_frame, Rng& g, Ctr<COUNT>& C) {
+  const uint32_t* __restrict__ N = P.nodes;
+  double closest = tmax;
+  bool hit = false;
+  d3 inv = mk(0., 0., 0.);
+  bool inv_ok = false;
+  for (;;) {
+    const uint32_t* X = N + node;
+    uint4 h = ld4u(X);
+    uint32_t type = h.x & 0xffu;
+    if (type == RTL_QUAD) {
+      double t;
+      if (quad_test<COUNT>(X, o, d, tmin, closest, t, C)) {
+        closest = t;
+        hit = true;
+        if (MAIN) {
+          hit_node = node;
+          hit_frame = frame;
+        }
+      }
+      node += RTL_QUAD_WORDS;
+    } else if (type == RTL_SPHERE) {
+      double t;
+      if (sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C)) {
+        closest = t;
+        hit = true;
+        if (MAIN) {
+          hit_node = node;
+          hit_frame = frame;
+        }
+      }
+      node += RTL_SPHERE_WORDS;
+    } else if (type == RTL_BVH) {
+      C.inc(RT_OP_AABB_TESTS);
+      if (!inv_ok) {
+        inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+        inv_ok = true;
+      }
+      node = aabb_test(X, o, inv, tmin, closest) ? node + RTL_BVH_WORDS : h.y;
+    } else if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y) {
+      C.inc(type == RTL_TRANSLATE ? RT_OP_TRANSLATE : RT_OP_ROTATE_Y);
+      xform_in(X, o, d);
+      if (type == RTL_ROTATE_Y) inv_ok = false;
+      frame = (int)node;
+      node += RTL_XFORM_WORDS;
+    } else if (type == RTL_EXIT) {
+      frame = (int)h.z;
+      frame_ray(N, frame, wo, wd, o, d);
+      inv_ok = false;
+      node += RTL_EXIT_WORDS;
+    } else if (MAIN && VOL && type == RTL_VOLUME) {
+      // ConstantMedium::hit constant_medium.rs:41-95
+      C.inc(RT_OP_VOLUME_TESTS);
+      double t1, t2;
+      uint32_t dn;
+      int df;
+      if (traverse<false, COUNT, false>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
+                                        -INFINITY, INFINITY, t1, dn, df, g, C) &&
+          traverse<false, COUNT, false>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
+                                        t1 + 0.0001, INFINITY, t2, dn, df, g, C)) {
+        if (t1 < tmin) t1 = tmin;
+        if (t2 > closest) t2 = closest;
+        if (t1 < t2) {
+          if (t1 < 0.0) t1 = 0.0;
+          double ray_length = sqrt(dot(d, d));
+          double dist_inside = (t2 - t1) * ray_length;
+          C.inc(RT_OP_VOLUME_DRAWS);
+          double hit_distance = ldd(X, 0) * log(rnd(g));
+          if (!(hit_distance > dist_inside)) {
+            closest = t1 + hit_distance / ray_length;
+            hit = true;
+            hit_node = node;
+            hit_frame = frame;
+          }
+        }
+      }
+      node = h.y;
+    } else if (type == RTL_END) {
+      break;
+    } else {
+      node = h.y;
+    }
+  }
+  t_out = closest;
+  return hit;
+}
+
+// ---------------------------------------------------------------- textures
+__device__ __forceinline__ int32_t f2i_sat(double f) {  // Rust `as i32`
+  if (f != f) return 0;
+  if (f >= 2147483648.0) return INT32_MAX;
+  if (f <= -2147483648.0) return INT32_MIN;
+  return (int32_t)f;
+}
+__device__ __forceinline__ uint32_t f2u_sat(double f) {  // Rust `as u32`
+  if (f != f || f <= 0.0) return 0u;
+  if (f >= 4294967296.0) return UINT32_MAX;
+  return (uint32_t)f;
+}
+
+// Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96 (out of line: only
+// noise-textured materials reach it)
+__device__ __noinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) {
+  const double* rv = reinterpret_cast<const double*>(T);
+  const uint8_t* px = T + 8192;
+  const uint8_t* py = px + 256;
+  const uint8_t* pz = py + 256;
+  double accum = 0.0, weight = 1.0;
+  for (int oct = 0; oct < 7; ++oct) {
+    double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    int32_t i = f2i_sat(fx), j = f2i_sat(fy), k = f2i_sat(fz);
+    double uu = u * u * (3.0 - 2.0 * u);
+    double vv = v * v * (3.0 - 2.0 * v);
+    double ww = w * w * (3.0 - 2.0 * w);
+    double acc = 0.0;
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+        for (int dk = 0; dk < 2; ++dk) {
+          uint32_t idx = px[(uint32_t)(i + di) & 255u] ^ py[(uint32_t)(j + dj) & 255u] ^
+                         pz[(uint32_t)(k + dk) & 255u];
+          double2 cxy = *reinterpret_cast<const double2*>(rv + 4 * idx);
+          d3 c = mk(cxy.x, cxy.y, rv[4 * idx + 2]);
+          double wi = di ? uu : 1.0 - uu;
+          double wj = dj ? vv : 1.0 - vv;
+          double wk = dk ? ww : 1.0 - ww;
+          d3 wv = mk(u - (double)di, v - (double)dj, w - (double)dk);
+          acc = fma(wi * wj * wk, dot(c, wv), acc);
+        }
+    accum = fma(weight, acc, accum);
+    weight *= 0.5;
+    p = p * 2.0;
+  }
+  return fabs(accum);
+}
+
+template <bool COUNT, bool TEX>
+__device__ d3 tex_value(const TraceParams& P, uint32_t id, double u, double v, d3 p,
+                        Ctr<COUNT>& C) {
+  if (!TEX) return ld3(P.texs + (size_t)id * RTL_TEX_WORDS, 0);
+  for (int guard = 0; guard < 65; ++guard) {
+    const uint32_t* t = P.texs + (size_t)id * RTL_TEX_WORDS;
+    uint4 h = ld4u(t);
+    if (h.x == RT_TEX_SOLID) return ld3(t, 0);
+    if (h.x == RT_TEX_CHECKER) {  // texture.rs:71-81
+      double is = ldd(t, 0);
+      int32_t x = f2i_sat(floor(is * p.x));
+      int32_t y = f2i_sat(floor(is * p.y));
+      int32_t z = f2i_sat(floor(is * p.z));
+      uint32_t sum = (uint32_t)x + (uint32_t)y + (uint32_t)z;
+      id = (sum & 1u) == 0u ? h.y : h.z;
+      continue;
+    }
+    if (h.x == RT_TEX_IMAGE) {  // texture.rs:95-107, rt_image.rs:37-46
+      int W = (int)h.y, H = (int)h.z;
+      if (H <= 0 || W <= 0) return mk(0., 1., 1.);
+      double cu = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);
+      double cv = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
+      uint32_t i = f2u_sat(cu * (double)W);
+      uint32_t j = f2u_sat(cv * (double)H);
+      uint32_t x = i < (uint32_t)(W - 1) ? i : (uint32_t)(W - 1);
+      uint32_t y = (uint32_t)H - j - 1u;
+      if (y > (uint32_t)(H - 1)) y = (uint32_t)(H - 1);
+      const uint8_t* px = P.texels + h.w + ((size_t)y * W + x) * 3;
+      const double cs = 1.0 / 255.0;
+      return mk((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+    }
+    if (h.x == RT_TEX_NOISE) {  // texture.rs:127-130
+      C.inc(RT_OP_NOISE_EVALS);
+      d3 s = p * ldd(t, 0);
+      double turb = perlin_turb(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
+      double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
+      return mk(k, k, k);
+    }
+    break;
+  }
+  return mk(0., 0., 0.);
+}
+
+// get_sphere_uv object.rs:114-120 (out of line: only image-textured spheres need it)
+__device__ __noinline__ void sphere_uv(d3 p, double& u, double& v) {
+  double theta = acos(-p.y);
+  double phi = atan2(-p.z, p.x) + kPi;
+  u = phi * (1.0 / kPi) * 0.5;
+  v = theta * (1.0 / kPi);
+}
+
+// ---------------------------------------------------------------- sampling
+struct Onb {
+  d3 u, v, w;
+};
+__device__ __forceinline__ Onb onb_from_w(d3 w) {  // onb.rs:32-47
+  Onb b;
+  d3 uw = unit_vector(w);
+  d3 a = fabs(uw.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
+  d3 v = unit_vector(cross(uw, a));
+  b.u = cross(uw, v);
+  b.v = v;
+  b.w = uw;
+  return b;
+}
+__device__ __forceinline__ d3 onb_local(const Onb& b, d3 a) {  // onb.rs:24-26
+  return vfma(a.x, b.u, vfma(a.y, b.v, b.w * a.z));
+}
+__device__ __forceinline__ d3 random_cosine_direction(Rng& g) {  // vec3.rs:240-250
+  double r1 = rnd(g);
+  double r2 = rnd(g);
+  double s, c;
+  sincos2pi(r1, &s, &c);
+  double sq = sqrt(r2);
+  return mk(c * sq, s * sq, sqrt(1.0 - r2));
+}
+__device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 231-238
+  for (;;) {
+    double x = rnd_pm1(g);
+    double y = rnd_pm1(g);
+    double z = rnd_pm1(g);
+    d3 p = mk(x, y, z);
+    if (dot(p, p) < 1.0) return unit_vector(p);
+  }
+}
+
+// Light-list PDF value (HittablePDF::value pdf.rs:91-93 -> HittableList::pdf_value
+// hittable.rs:115-124 -> Quad/Sphere::pdf_value object.rs:492-501, 190-202).
+template <bool COUNT>
+__device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>& C) {
+  double sum = 0.0;
+  for (uint32_t i = 0; i < P.n_lights; ++i) {
+    const uint32_t* L = P.lights + P.light_offs[i];
+    uint32_t type = L[0] & 0xffu;
+    double pv = 0.0;
+    if (type == RTL_QUAD) {
+      C.inc(RT_OP_LIGHT_PDF_QUAD);
+      double t;
+      if (quad_test<COUNT>(L, origin, dir, 0.001, INFINITY, t, C)) {
+        double len2 = dot(dir, dir);
+        double dist2 = (t * t) * len2;
+        double cosine = fabs(dot(dir, ld3(L, 0)) / sqrt(len2));
+        pv = dist2 / (cosine * ldd(L, 7));
+      }
+    } else if (type == RTL_SPHERE) {
+      C.inc(RT_OP_LIGHT_PDF_SPHERE);
+      double t;
+      if (sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, INFINITY, t, C)) {
+        d3 c = ld3(L, 0);
+        double r = ldd(L, 3);
+        d3 cmo = c - origin;
+        double cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
+        double solid = 2.0 * kPi * (1.0 - cos_max);
+        pv = 1.0 / solid;
+      }
+    }
+    sum = i == 0 ? pv : sum + pv;
+  }
+  return P.lights_is_list ? sum * (1.0 / (double)P.n_lights) : sum;
+}
+
+// Light-list generate (HittablePDF::generate pdf.rs:95-97 -> HittableList::random
+// hittable.rs:126-129 -> Quad::random object.rs:503-506 / Sphere::random 204-212).
+__device__ d3 light_random(const TraceParams& P, d3 origin, Rng& g) {
+  uint32_t i = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
+  const uint32_t* L = P.lights + P.light_offs[i];
+  uint32_t type = L[0] & 0xffu;
+  if (type == RTL_QUAD) {
+    double a = rnd(g);
+    double b = rnd(g);
+    d3 p = vfma(b, ld3(L, 16), vfma(a, ld3(L, 12), ld3(L, 4)));
+    return p - origin;
+  }
+  if (type == RTL_SPHERE) {
+    d3 c = ld3(L, 0);
+    double r = ldd(L, 3);
+    d3 direction = c - origin;
+    double dist2 = dot(direction, direction);
+    Onb b = onb_from_w(direction);
+    double r1 = rnd(g), r2 = rnd(g);  // random_to_sphere object.rs:122-132
+    double z = fma(r2, sqrt(1.0 - r * r / dist2) - 1.0, 1.0);
+    double s, cc;
+    sincos2pi(r1, &s, &cc);
+    double sq = sqrt(fma(-z, z, 1.0));
+    return onb_local(b, mk(cc * sq, s * sq, z));
+  }
+  return mk(1., 0., 0.);
+}
+
+// ---------------------------------------------------------------- the path kernel
+// VOL: scene has ConstantMedium nodes; TEX: some material reads a non-solid texture.
+template <bool COUNT, bool VOL, bool TEX>
+__global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
+  __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
+  if (COUNT) {
+    for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
+    __syncthreads();
+  }
+  Ctr<COUNT> C;
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int sjl = wave % P.n_sj;
+  const int tile = wave / P.n_sj;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const int x = tx * kWaveTile + (lane & 7);
+  const int kr = ty * kWaveTile + (lane >> 3);
+  const bool active = x < P.W && kr < P.n_rows;
+  const int y = P.row_begin + kr * P.row_step;
+  const uint32_t pixel = (uint32_t)(y * P.W + x);
+  const int s_j = P.sj0 + sjl;
+  const bool have_lights = P.n_lights > 0;
+  const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
+
+  d3 row = mk(0., 0., 0.);
+  d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
+  double tm = 0.;
+  int depth = 0;
+  int s_i = 0;
+  bool alive = false;
+  Rng g = {0u, 0u, 0u, 0u};
+
+  for (;;) {
+    if (!alive) {
+      if (!active || s_i >= P.sqrt_spp) break;
+      // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
+      g = rng_seed(P.seed_lo, P.seed_hi, pixel, (uint32_t)(s_j * P.sqrt_spp + s_i));
+      C.inc(RT_OP_SAMPLES);
+      d3 pc = vfma((double)y, arr3(P.dv), vfma((double)x, arr3(P.du), arr3(P.p00)));
+      double px = fma(P.rs, (double)s_i + rnd(g), -0.5);
+      double py = fma(P.rs, (double)s_j + rnd(g), -0.5);
+      d3 ps = pc + vfma(px, arr3(P.du), arr3(P.dv) * py);
+      d3 origin = arr3(P.center);
+      if (P.defocus) {
+        for (;;) {
+          double dx = rnd_pm1(g);
+          double dy = rnd_pm1(g);
+          if (fma(dx, dx, dy * dy) < 1.0) {
+            origin = vfma(dy, arr3(P.ddv), vfma(dx, arr3(P.ddu), arr3(P.center)));
+            break;
+          }
+        }
+      }
+      ro = origin;
+      rd = ps - origin;
+      tm = rnd(g);
+      beta = mk(1., 1., 1.);
+      Lp = mk(0., 0., 0.);
+      depth = P.max_depth;
+      alive = true;
+      ++s_i;
+    }
+    if (depth <= 0) {  // ray_color depth guard render.rs:260-262
+      C.inc(RT_OP_DEPTH_CUTOFF);
+      row = row + Lp;
+      alive = false;
+      continue;
+    }
+    C.inc(RT_OP_WORLD_QUERIES);
+    double t;
+    uint32_t hn = 0;
+    int hf = -1;
+    if (!traverse<true, COUNT, VOL>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
+                                    hf, g, C)) {
+      C.inc(RT_OP_MISSES);  // background render.rs:298-309
+      Lp = Lp + beta * arr3(P.bg);
+      row = row + Lp;
+      alive = false;
+      continue;
+    }
+    // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
+    const uint32_t* X = P.nodes + hn;
+    uint32_t type = X[0] & 0xffu;
+    d3 o, d;
+    frame_ray(P.nodes, hf, ro, rd, o, d);
+    d3 p = vfma(t, d, o);
+    d3 normal;
+    bool front = true;
+    double u = 0., v = 0.;
+    const uint32_t* M = P.mats + (size_t)X[2] * RTL_MAT_WORDS;
+    uint4 mh = ld4u(M);
+    const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
+    if (type == RTL_QUAD) {
+      d3 n = ld3(X, 0);
+      front = dot(d, n) < 0.0;  // set_face_normal hittable.rs:22-37
+      normal = front ? n : -n;
+      if (needs_uv) {
+        d3 pq = p - ld3(X, 4);
+        d3 w = ld3(X, 8);
+        u = dot(w, cross(pq, ld3(X, 16)));
+        v = dot(w, cross(ld3(X, 12), pq));
+      }
+    } else if (type == RTL_SPHERE) {
+      d3 c = ld3(X, 0);
+      if (X[3]) c = vfma(tm, ld3(X, 4), c);
+      d3 outward = (p - c) * ldd(X, 7);
+      front = dot(d, outward) < 0.0;
+      normal = front ? outward : -outward;
+      if (needs_uv) sphere_uv(outward, u, v);
+    } else {  // volume (constant_medium.rs:82-90)
+      normal = mk(1., 0., 0.);
+    }
+    if (hf >= 0) {  // back to world space, innermost transform first
+      uint4 fh = ld4u(P.nodes + hf);
+      uint4 ch = ld4u(P.nodes + hf + 4);
+      const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+      for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
+        if ((uint32_t)k < fh.z) xform_out(P.nodes + c4[k], p, normal);
+    }
+    const uint32_t kind = mh.x & 0xffu;
+    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
+      C.inc(RT_OP_EMISSIVE_HITS);
+      if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, mh.y, u, v, p, C), Lp);
+      row = row + Lp;
+      alive = false;
+      continue;
+    }
+    if (kind == RT_MAT_METAL) {  // material.rs:124-134
+      C.inc(RT_OP_METAL);
+      d3 reflected = reflect(unit_vector(rd), normal);
+      d3 ruv = random_unit_vector(g);
+      reflected = vfma(ldd(M, 3), ruv, unit_vector(reflected));
+      beta = beta * ld3(M, 0);
+      ro = p;
+      rd = reflected;
+      --depth;
+      continue;
+    }
+    if (kind == RT_MAT_DIELECTRIC) {  // material.rs:166-191
+      C.inc(RT_OP_DIELECTRIC);
+      double ir = ldd(M, 3);
+      double ratio = front ? 1.0 / ir : ir;
+      d3 ud = unit_vector(rd);
+      double cos_t = fmin(dot(-ud, normal), 1.0);
+      double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
+      bool refl = ratio * sin_t > 1.0;
+      if (!refl) {
+        double r0 = (1.0 - ratio) / (1.0 + ratio);
+        r0 = r0 * r0;
+        double xx = 1.0 - cos_t;
+        double x2 = xx * xx;
+        refl = fma(1.0 - r0, x2 * x2 * xx, r0) > rnd(g);
+      }
+      rd = refl ? reflect(ud, normal) : refract(ud, normal, ratio);
+      beta = beta * ld3(M, 0);
+      ro = p;
+      --depth;
+      continue;
+    }
+    // Lambertian / Isotropic: mixture-PDF branch render.rs:278-292
+    const bool iso = kind == RT_MAT_ISOTROPIC;
+    C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
+    d3 atten = tex_value<COUNT, TEX>(P, mh.y, u, v, p, C);
+    Onb uvw;
+    if (!iso) uvw = onb_from_w(normal);  // CosinePDF::new pdf.rs:58-62
+    d3 dir;
+    bool light_branch = false;
+    if (have_lights) light_branch = rnd(g) < 0.5;  // MixturePDF::generate pdf.rs:120-126
+    if (light_branch) {
+      C.inc(RT_OP_LIGHT_GEN);
+      dir = light_random(P, p, g);
+    } else {
+      C.inc(RT_OP_COSINE_GEN);
+      dir = iso ? random_unit_vector(g) : onb_local(uvw, random_cosine_direction(g));
+    }
+    double mat_pdf, s_pdf;
+    if (iso) {
+      mat_pdf = 1.0 / (4.0 * kPi);                   // SpherePDF::value pdf.rs:47-49
+      s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
+    } else {
+      d3 udir = unit_vector(dir);
+      double cv = dot(udir, uvw.w) / kPi;            // CosinePDF::value pdf.rs:69-73
+      mat_pdf = cv > 0.0 ? cv : 0.0;
+      double cs = dot(normal, udir);                 // Lambertian::scattering_pdf 100-108
+      s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
+    }
+    double pdf_val = mat_pdf;
+    if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, C), 0.5 * mat_pdf);  // pdf.rs:116
+    beta = beta * (atten * (s_pdf / pdf_val));
+    ro = p;
+    rd = dir;
+    --depth;
+  }
+  if (active) {
+    float* out = P.partial + ((size_t)(sjl * P.n_rows + kr) * P.W + x) * 3;
+    out[0] = (float)row.x;
+    out[1] = (float)row.y;
+    out[2] = (float)row.z;
+  }
+  if (COUNT) {
+    C.flush(sh_ops);
+    __syncthreads();
+    for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x)
+      if (sh_ops[k]) atomicAdd(&P.ops[k], (unsigned long long)sh_ops[k]);
+  }
+}
+
+// Sum the per-stratum-row partials in s_j order (render.rs:185-189 accumulation), then add
+// into (or overwrite) the caller's raw-sum framebuffer.
+__global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ partial,
+                                                 float* __restrict__ accum, int n_px, int n_sj,
+                                                 int overwrite) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_px * 3) return;
+  double s = 0.0;
+  for (int k = 0; k < n_sj; ++k) s += (double)partial[(size_t)k * n_px * 3 + i];
+  accum[i] = overwrite ? (float)s : (float)((double)accum[i] + s);
+}
+
+// ---------------------------------------------------------------- host side
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err(RT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+}  // namespace
+
+struct rt_scene {
+  int device = 0;
+  rtl_scene_header hdr{};
+  uint8_t* dev = nullptr;  // one allocation for all tables
+  uint64_t dev_bytes = 0;
+  const uint32_t *nodes = nullptr, *mats = nullptr, *texs = nullptr, *lights = nullptr,
+                 *light_offs = nullptr;
+  const uint8_t *perlin = nullptr, *texels = nullptr;
+  float* partial = nullptr;
+  size_t partial_bytes = 0;
+  unsigned long long* ops = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::mutex mu;
+};
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(int* count) {
+  if (!count) return set_err(RT_ERR_INVALID_ARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return RT_OK;
+}
+
+int rt_scene_validate(const rt_scene_blob* blob) {
+  rtf::FlatScene F;
+  std::string err;
+  int rc = rtf::flatten(blob, &F, &err);
+  if (rc != RT_OK) return set_err(rc, err);
+  return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
+  if (!out) return set_err(RT_ERR_INVALID_ARG, "null out");
+  *out = nullptr;
+  rtf::FlatScene F;
+  std::string err;
+  int rc = rtf::flatten(blob, &F, &err);
+  if (rc != RT_OK) return set_err(rc, err);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_err(RT_ERR_NO_DEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return set_err(RT_ERR_INVALID_ARG, "bad device ordinal");
+  HIP_TRY(hipSetDevice(device));
+  // pack tables into one 256-B aligned allocation
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t o_nodes = 0, s_nodes = F.nodes.size() * 4;
+  size_t o_mats = al(o_nodes + s_nodes), s_mats = F.mats.size() * 4;
+  size_t o_texs = al(o_mats + s_mats), s_texs = F.texs.size() * 4;
+  size_t o_perl = al(o_texs + s_texs), s_perl = F.perlin.size();
+  size_t o_lig = al(o_perl + s_perl), s_lig = F.lights.size() * 4;
+  size_t o_loff = al(o_lig + s_lig), s_loff = F.light_offs.size() * 4;
+  size_t o_tx = al(o_loff + s_loff), s_tx = F.texels.size();
+  size_t total = al(o_tx + s_tx) + 256;
+  std::vector<uint8_t> host(total, 0);
+  auto cp = [&](size_t off, const void* src, size_t n) {
+    if (n) std::memcpy(host.data() + off, src, n);
+  };
+  cp(o_nodes, F.nodes.data(), s_nodes);
+  cp(o_mats, F.mats.data(), s_mats);
+  cp(o_texs, F.texs.data(), s_texs);
+  cp(o_perl, F.perlin.data(), s_perl);
+  cp(o_lig, F.lights.data(), s_lig);
+  cp(o_loff, F.light_offs.data(), s_loff);
+  cp(o_tx, F.texels.data(), s_tx);
+  rt_scene* sc = new rt_scene();
+  sc->device = device;
+  sc->hdr = F.hdr;
+  hipError_t e = hipMalloc(&sc->dev, total);
+  if (e == hipSuccess) e = hipMemcpy(sc->dev, host.data(), total, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&sc->ops, sizeof(unsigned long long) * 32);
+  if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
+  if (e != hipSuccess) {
+    rt_scene_destroy(sc);
+    return set_err(RT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+  }
+  sc->dev_bytes = total;
+  sc->nodes = (const uint32_t*)(sc->dev + o_nodes);
+  sc->mats = (const uint32_t*)(sc->dev + o_mats);
+  sc->texs = (const uint32_t*)(sc->dev + o_texs);
+  sc->perlin = sc->dev + o_perl;
+  sc->lights = (const uint32_t*)(sc->dev + o_lig);
+  sc->light_offs = (const uint32_t*)(sc->dev + o_loff);
+  sc->texels = sc->dev + o_tx;
+  *out = sc;
+  return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* sc) {
+  if (!sc) return;
+  (void)hipSetDevice(sc->device);
+  if (sc->dev) (void)hipFree(sc->dev);
+  if (sc->partial) (void)hipFree(sc->partial);
+  if (sc->ops) (void)hipFree(sc->ops);
+  if (sc->ev0) (void)hipEventDestroy(sc->ev0);
+  if (sc->ev1) (void)hipEventDestroy(sc->ev1);
+  delete sc;
+}
+
+uint64_t rt_scene_device_bytes(const rt_scene* sc) { return sc ? sc->dev_bytes : 0; }
+
+int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
+                     float* accum, void* stream_v, rt_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!sc || !cam || !opts || !accum) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  const int W = cam->image_width, S = cam->sqrt_spp;
+  if (W <= 0 || cam->image_height <= 0 || S <= 0 || cam->max_depth < 0 || opts->n_rows < 0 ||
+      opts->row_step <= 0 || opts->row_begin < 0)
+    return set_err(RT_ERR_INVALID_ARG, "bad camera or row range");
+  if (opts->n_rows > 0 &&
+      (int64_t)opts->row_begin + (int64_t)(opts->n_rows - 1) * opts->row_step >= cam->image_height)
+    return set_err(RT_ERR_INVALID_ARG, "row range outside the image");
+  if ((int64_t)W * cam->image_height >= (1ll << 32) || (int64_t)S * S >= (1ll << 32))
+    return set_err(RT_ERR_UNSUPPORTED, "image or spp too large for 32-bit pixel/sample keys");
+  const int sj0 = opts->sj_count > 0 ? opts->sj_begin : 0;
+  const int n_sj = opts->sj_count > 0 ? opts->sj_count : S;
+  if (sj0 < 0 || sj0 + n_sj > S) return set_err(RT_ERR_INVALID_ARG, "bad stratum range");
+  if (sc->hdr.n_lights == 0 && (opts->flags & RT_FLAG_SEMANTICS_REFERENCE) && sc->hdr.pdf_materials)
+    return set_err(RT_ERR_EMPTY_LIGHTS,
+                   "empty light list with a diffuse/volume material: the reference panics "
+                   "(hittable.rs:115-129)");
+  std::lock_guard<std::mutex> lock(sc->mu);
+  hipStream_t stream = (hipStream_t)stream_v;
+  HIP_TRY(hipSetDevice(sc->device));
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  const size_t n_px = (size_t)opts->n_rows * W;
+  if (n_px == 0) return RT_OK;
+  const size_t need = n_px * 3 * sizeof(float) * (size_t)n_sj;
+  if (need > sc->partial_bytes) {
+    if (sc->partial) HIP_TRY(hipFree(sc->partial));
+    sc->partial = nullptr;
+    sc->partial_bytes = 0;
+    HIP_TRY(hipMalloc(&sc->partial, need));
+    sc->partial_bytes = need;
+  }
+  TraceParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.nodes = sc->nodes;
+  P.mats = sc->mats;
+  P.texs = sc->texs;
+  P.perlin = sc->perlin;
+  P.lights = sc->lights;
+  P.light_offs = sc->light_offs;
+  P.texels = sc->texels;
+  P.partial = sc->partial;
+  P.ops = sc->ops;
+  P.root = sc->hdr.root;
+  P.n_lights = sc->hdr.n_lights;
+  P.lights_is_list = sc->hdr.lights_is_list;
+  P.flags = opts->flags;
+  for (int k = 0; k < 3; ++k) {
+    P.center[k] = cam->center[k];
+    P.p00[k] = cam->pixel00_loc[k];
+    P.du[k] = cam->pixel_delta_u[k];
+    P.dv[k] = cam->pixel_delta_v[k];
+    P.ddu[k] = cam->defocus_disk_u[k];
+    P.ddv[k] = cam->defocus_disk_v[k];
+    P.bg[k] = cam->background[k];
+  }
+  P.rs = cam->recip_sqrt_spp;
+  P.defocus = cam->defocus_angle > 0.0;
+  P.W = W;
+  P.n_rows = opts->n_rows;
+  P.row_begin = opts->row_begin;
+  P.row_step = opts->row_step;
+  P.sqrt_spp = S;
+  P.sj0 = sj0;
+  P.n_sj = n_sj;
+  P.max_depth = cam->max_depth;
+  P.seed_lo = (uint32_t)opts->seed;
+  P.seed_hi = (uint32_t)(opts->seed >> 32);
+  P.tiles_x = (W + kWaveTile - 1) / kWaveTile;
+  const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
+  const int64_t waves = (int64_t)P.tiles_x * tiles_y * n_sj;
+  const int64_t blocks = (waves + (kBlock / 64) - 1) / (kBlock / 64);
+  if (blocks > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+  const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
+  if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
+  if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
+  const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
+  auto kern = count ? (vol ? (tex ? rt_trace<true, true, true> : rt_trace<true, true, false>)
+                           : (tex ? rt_trace<true, false, true> : rt_trace<true, false, false>))
+                    : (vol ? (tex ? rt_trace<false, true, true> : rt_trace<false, true, false>)
+                           : (tex ? rt_trace<false, false, true> : rt_trace<false, false, false>));
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
+  HIP_TRY(hipGetLastError());
+  if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));
+  const int n3 = (int)(n_px * 3);
+  hipLaunchKernelGGL(rt_reduce, dim3((n3 + 255) / 256), dim3(256), 0, stream, sc->partial, accum,
+                     (int)n_px, n_sj, (opts->flags & RT_FLAG_OVERWRITE) ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+  if (stats) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, sc->ev0, sc->ev1));
+    stats->ms_kernel = ms;
+    stats->samples = (uint64_t)n_px * (uint64_t)n_sj * (uint64_t)S;
+    if (count) {
+      unsigned long long h[32];
+      HIP_TRY(hipMemcpy(h, sc->ops, sizeof(h), hipMemcpyDeviceToHost));
+      for (int k = 0; k < 32; ++k) stats->ops[k] = h[k];
+    }
+    stats->ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return RT_OK;
+}
+
+int rt_render(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts, float* accum,
+              rt_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!sc || !cam || !opts || !accum) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  if (opts->n_rows < 0 || cam->image_width <= 0) return set_err(RT_ERR_INVALID_ARG, "bad size");
+  HIP_TRY(hipSetDevice(sc->device));
+  size_t bytes = (size_t)opts->n_rows * cam->image_width * 3 * sizeof(float);
+  if (bytes == 0) return RT_OK;
+  float* d = nullptr;
+  HIP_TRY(hipMalloc(&d, bytes));
+  hipError_t e = (opts->flags & RT_FLAG_OVERWRITE) ? hipSuccess
+                                                   : hipMemcpy(d, accum, bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return set_err(RT_ERR_HIP, std::string("upload accum: ") + hipGetErrorString(e));
+  }
+  rt_stats local;
+  int rc = rt_render_device(sc, cam, opts, d, nullptr, stats ? stats : &local);
+  if (rc == RT_OK) {
+    e = hipMemcpy(accum, d, bytes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = set_err(RT_ERR_HIP, std::string("download accum: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(d);
+  if (rc == RT_OK && stats)
+    stats->ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
+                   float* accum, rt_stats* stats) {
+  if (!opts) return set_err(RT_ERR_INVALID_ARG, "null opts");
+  rt_scene* sc = nullptr;
+  int rc = rt_scene_create(blob, opts->device, &sc);
+  if (rc != RT_OK) return rc;
+  rc = rt_render(sc, cam, opts, accum, stats);
+  rt_scene_destroy(sc);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,478 @@
+// rt_flatten.cpp — validate an rt_scene_blob and flatten it for the device.
+//
+// Input: the prefix-serialised object tree of the reference scene (HittableList / BvhNode /
+// Sphere / Quad / Translate / RotateY / ConstantMedium, include/rt_mi355x.h). Output: one
+// threaded pre-order word array (rt_layout.h) whose sequential walk reproduces the reference's
+// recursive visiting order (hittable.rs:88-109, 216-236; transform.rs:57-135;
+// constant_medium.rs:41-95), plus fp32 material / texture / Perlin / light tables.
+// Shared subtrees (Arc<Object> clones, BVH span-1 duplicate leaves hittable.rs:161-162) are
+// emitted once per reference, exactly as often as the reference would visit them.
+#include "rt_flatten.hpp"
+
+#include <cstring>
+#include <memory>
+
+namespace rtf {
+
+namespace {
+
+struct Node {
+  int tag = 0;
+  int64_t mat = -1;
+  int64_t moving = 0;
+  double f[32] = {0};  // tag-specific payload (see read_node)
+  double bbox[6] = {0};
+  std::vector<std::unique_ptr<Node>> kids;
+};
+
+struct Reader {
+  const uint64_t* s;
+  uint64_t n, pos;
+  bool err = false;
+  std::string msg;
+  int64_t i() {
+    if (pos >= n) return fail("truncated blob"), 0;
+    return (int64_t)s[pos++];
+  }
+  double f() {
+    if (pos >= n) return fail("truncated blob"), 0.0;
+    double d;
+    std::memcpy(&d, &s[pos++], 8);
+    return d;
+  }
+  void fail(const std::string& m) {
+    if (!err) msg = m;
+    err = true;
+  }
+};
+
+std::unique_ptr<Node> read_node(Reader& r, int depth) {
+  if (depth > 256) {
+    r.fail("object tree deeper than 256");
+    return nullptr;
+  }
+  auto nd = std::make_unique<Node>();
+  nd->tag = (int)r.i();
+  auto bbox = [&]() {
+    for (int k = 0; k < 6; ++k) nd->bbox[k] = r.f();
+  };
+  switch (nd->tag) {
+    case RT_OBJ_LIST: {
+      int64_t cnt = r.i();
+      bbox();
+      if (cnt < 0 || cnt > (1 << 24)) {
+        r.fail("bad list length");
+        return nullptr;
+      }
+      for (int64_t k = 0; k < cnt && !r.err; ++k) nd->kids.push_back(read_node(r, depth + 1));
+      break;
+    }
+    case RT_OBJ_BVH:
+      bbox();
+      nd->kids.push_back(read_node(r, depth + 1));
+      if (!r.err) nd->kids.push_back(read_node(r, depth + 1));
+      break;
+    case RT_OBJ_SPHERE:  // mat moving c3 radius cvec3
+      nd->mat = r.i();
+      nd->moving = r.i();
+      for (int k = 0; k < 7; ++k) nd->f[k] = r.f();
+      bbox();
+      break;
+    case RT_OBJ_QUAD:  // mat q3 u3 v3 n3 w3 d area
+      nd->mat = r.i();
+      for (int k = 0; k < 17; ++k) nd->f[k] = r.f();
+      bbox();
+      break;
+    case RT_OBJ_TRANSLATE:  // offset3
+      for (int k = 0; k < 3; ++k) nd->f[k] = r.f();
+      bbox();
+      nd->kids.push_back(read_node(r, depth + 1));
+      break;
+    case RT_OBJ_ROTATE_Y:  // sin cos
+      nd->f[0] = r.f();
+      nd->f[1] = r.f();
+      bbox();
+      nd->kids.push_back(read_node(r, depth + 1));
+      break;
+    case RT_OBJ_VOLUME:  // mat neg_inv_density
+      nd->mat = r.i();
+      nd->f[0] = r.f();
+      bbox();
+      nd->kids.push_back(read_node(r, depth + 1));
+      break;
+    default:
+      r.fail("unknown object tag " + std::to_string(nd->tag));
+      return nullptr;
+  }
+  if (r.err) return nullptr;
+  for (auto& k : nd->kids)
+    if (!k) {
+      r.fail("bad child");
+      return nullptr;
+    }
+  return nd;
+}
+
+// write an f64 payload value at double index k of the node starting at word p
+inline void putd(std::vector<uint32_t>& w, size_t p, int k, double d) {
+  std::memcpy(&w[p + 4 + 2 * (size_t)k], &d, 8);
+}
+
+struct Emitter {
+  std::vector<uint32_t>& w;
+  int64_t n_mats;
+  std::string err;
+  int status = RT_OK;
+  uint32_t max_chain = 0;
+  bool has_bvh = false, has_volume = false;
+  size_t last_exit_end = (size_t)-1;  // end position of the most recent EXIT node
+  size_t last_skip_target = (size_t)-1;
+
+  explicit Emitter(std::vector<uint32_t>& words, int64_t nm) : w(words), n_mats(nm) {}
+
+  void fail(int code, const std::string& m) {
+    if (status == RT_OK) {
+      status = code;
+      err = m;
+    }
+  }
+  size_t push(uint32_t type, size_t n_words) {
+    size_t pos = w.size();
+    w.resize(pos + n_words, 0u);
+    w[pos] = type;
+    w[pos + 1] = 0xffffffffu;
+    return pos;
+  }
+  void set_skip(size_t pos) {
+    w[pos + 1] = (uint32_t)w.size();
+    last_skip_target = w.size();
+  }
+  bool check_mat(int64_t m) {
+    if (m < 0 || m >= n_mats) {
+      fail(RT_ERR_BAD_BLOB, "material index out of range");
+      return false;
+    }
+    return true;
+  }
+  void quad(const Node& n, bool light) {
+    if (!check_mat(n.mat) && !light) return;
+    size_t p = push(RTL_QUAD, RTL_QUAD_WORDS);
+    const double* f = n.f;  // q 0-2, u 3-5, v 6-8, n 9-11, w 12-14, d 15, area 16
+    w[p + 2] = (uint32_t)(n.mat < 0 ? 0 : n.mat);
+    putd(w, p, 0, f[9]), putd(w, p, 1, f[10]), putd(w, p, 2, f[11]), putd(w, p, 3, f[15]);
+    putd(w, p, 4, f[0]), putd(w, p, 5, f[1]), putd(w, p, 6, f[2]), putd(w, p, 7, f[16]);
+    putd(w, p, 8, f[12]), putd(w, p, 9, f[13]), putd(w, p, 10, f[14]);
+    putd(w, p, 12, f[3]), putd(w, p, 13, f[4]), putd(w, p, 14, f[5]);
+    putd(w, p, 16, f[6]), putd(w, p, 17, f[7]), putd(w, p, 18, f[8]);
+  }
+  void sphere(const Node& n, bool light) {
+    if (!check_mat(n.mat) && !light) return;
+    size_t p = push(RTL_SPHERE, RTL_SPHERE_WORDS);
+    const double* f = n.f;  // c 0-2, radius 3, cvec 4-6
+    w[p + 2] = (uint32_t)(n.mat < 0 ? 0 : n.mat);
+    w[p + 3] = n.moving ? 1u : 0u;
+    putd(w, p, 0, f[0]), putd(w, p, 1, f[1]), putd(w, p, 2, f[2]), putd(w, p, 3, f[3]);
+    putd(w, p, 4, f[4]), putd(w, p, 5, f[5]), putd(w, p, 6, f[6]);
+    putd(w, p, 7, 1.0 / f[3]);  // outward = (p - c) * (1/r)
+  }
+  void exit_to(int parent) {
+    // Consecutive EXITs collapse into one (restoring straight to the outermost parent) unless
+    // a skip link targets the position between them.
+    if (last_exit_end == w.size() && last_skip_target != w.size()) {
+      w[w.size() - RTL_EXIT_WORDS + 2] = (uint32_t)parent;
+      return;
+    }
+    size_t p = push(RTL_EXIT, RTL_EXIT_WORDS);
+    w[p + 2] = (uint32_t)parent;
+    last_exit_end = w.size();
+  }
+  void emit(const Node& n, int frame, std::vector<uint32_t>& chain, bool in_volume) {
+    if (status != RT_OK) return;
+    switch (n.tag) {
+      case RT_OBJ_LIST:
+        for (auto& k : n.kids) emit(*k, frame, chain, in_volume);
+        break;
+      case RT_OBJ_BVH: {
+        has_bvh = true;
+        size_t p = push(RTL_BVH, RTL_BVH_WORDS);
+        for (int k = 0; k < 6; ++k) putd(w, p, k, n.bbox[k]);
+        emit(*n.kids[0], frame, chain, in_volume);
+        emit(*n.kids[1], frame, chain, in_volume);
+        set_skip(p);
+        break;
+      }
+      case RT_OBJ_QUAD: quad(n, false); break;
+      case RT_OBJ_SPHERE: sphere(n, false); break;
+      case RT_OBJ_TRANSLATE:
+      case RT_OBJ_ROTATE_Y: {
+        if (chain.size() >= RTL_MAX_CHAIN) {
+          fail(RT_ERR_UNSUPPORTED, "more than 4 nested Translate/RotateY instances");
+          return;
+        }
+        bool tr = n.tag == RT_OBJ_TRANSLATE;
+        size_t p = push(tr ? RTL_TRANSLATE : RTL_ROTATE_Y, RTL_XFORM_WORDS);
+        chain.push_back((uint32_t)p);
+        if (chain.size() > max_chain) max_chain = (uint32_t)chain.size();
+        w[p + 2] = (uint32_t)chain.size();
+        for (size_t k = 0; k < chain.size(); ++k) w[p + 4 + k] = chain[k];
+        if (tr) {
+          putd(w, p, 2, n.f[0]), putd(w, p, 3, n.f[1]), putd(w, p, 4, n.f[2]);
+        } else {
+          putd(w, p, 2, n.f[0]), putd(w, p, 3, n.f[1]);
+        }
+        emit(*n.kids[0], (int)p, chain, in_volume);
+        chain.pop_back();
+        exit_to(frame);
+        w[p + 1] = (uint32_t)w.size();
+        break;
+      }
+      case RT_OBJ_VOLUME: {
+        if (in_volume) {
+          fail(RT_ERR_UNSUPPORTED, "ConstantMedium nested inside a ConstantMedium boundary");
+          return;
+        }
+        if (!check_mat(n.mat)) return;
+        has_volume = true;
+        size_t p = push(RTL_VOLUME, RTL_VOLUME_WORDS);
+        w[p + 2] = (uint32_t)n.mat;
+        putd(w, p, 0, n.f[0]);
+        emit(*n.kids[0], frame, chain, true);
+        push(RTL_END, RTL_END_WORDS);
+        set_skip(p);
+        break;
+      }
+    }
+  }
+};
+
+bool tex_needs_uv(const std::vector<uint32_t>& texs, uint32_t id, int depth) {
+  if (depth > 64) return false;
+  const uint32_t* t = &texs[(size_t)id * RTL_TEX_WORDS];
+  if (t[0] == RT_TEX_IMAGE) return t[1] > 0 && t[2] > 0;
+  if (t[0] == RT_TEX_CHECKER) return tex_needs_uv(texs, t[1], depth + 1) || tex_needs_uv(texs, t[2], depth + 1);
+  return false;
+}
+
+}  // namespace
+
+int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
+  if (!blob || !blob->slots || blob->n_slots < RT_BLOB_HEADER_SLOTS) {
+    *err = "null or short blob";
+    return RT_ERR_BAD_BLOB;
+  }
+  const uint64_t* s = blob->slots;
+  if (s[0] != RT_BLOB_MAGIC || s[1] != RT_BLOB_VERSION || s[2] != blob->n_slots) {
+    *err = "bad blob magic/version/size";
+    return RT_ERR_BAD_BLOB;
+  }
+  uint64_t n = blob->n_slots;
+  uint64_t n_tex = s[3], tex_off = s[4], n_mat = s[5], mat_off = s[6], n_perl = s[7],
+           perl_off = s[8], world_off = s[9];
+  int64_t lights_off = (int64_t)s[10];
+  uint64_t n_texel = s[11];
+  if (n_tex > (1u << 20) || n_mat > (1u << 20) || n_perl > 4096 ||
+      tex_off + n_tex * RT_TEX_SLOTS > n || mat_off + n_mat * RT_MAT_SLOTS > n ||
+      perl_off + n_perl * RT_PERLIN_SLOTS > n || world_off >= n ||
+      (lights_off >= 0 && (uint64_t)lights_off >= n) || n_texel != blob->n_texels ||
+      (n_texel > 0 && !blob->texels)) {
+    *err = "blob header out of range";
+    return RT_ERR_BAD_BLOB;
+  }
+  FlatScene& F = *out;
+  F = FlatScene();
+  auto setd = [](uint32_t* o, int k, double d) { std::memcpy(o + 4 + 2 * k, &d, 8); };
+  auto rd_f = [&](uint64_t i) {
+    double d;
+    std::memcpy(&d, &s[i], 8);
+    return d;
+  };
+  // textures
+  F.texs.assign(n_tex * RTL_TEX_WORDS, 0u);
+  for (uint64_t t = 0; t < n_tex; ++t) {
+    uint64_t b = tex_off + t * RT_TEX_SLOTS;
+    uint32_t* o = &F.texs[t * RTL_TEX_WORDS];
+    int64_t kind = (int64_t)s[b];
+    o[0] = (uint32_t)kind;
+    switch (kind) {
+      case RT_TEX_SOLID:
+        setd(o, 0, rd_f(b + 1)), setd(o, 1, rd_f(b + 2)), setd(o, 2, rd_f(b + 3));
+        break;
+      case RT_TEX_CHECKER: {
+        int64_t e = (int64_t)s[b + 2], d = (int64_t)s[b + 3];
+        if (e < 0 || d < 0 || (uint64_t)e >= n_tex || (uint64_t)d >= n_tex) {
+          *err = "checker texture index out of range";
+          return RT_ERR_BAD_BLOB;
+        }
+        setd(o, 0, rd_f(b + 1)), o[1] = (uint32_t)e, o[2] = (uint32_t)d;
+        break;
+      }
+      case RT_TEX_IMAGE: {
+        int64_t w = (int64_t)s[b + 1], h = (int64_t)s[b + 2], off = (int64_t)s[b + 3];
+        if (w < 0 || h < 0 || off < 0 || (w > 0 && h > 0 && (uint64_t)(off + w * h * 3) > n_texel)) {
+          *err = "image texture out of range";
+          return RT_ERR_BAD_BLOB;
+        }
+        o[1] = (uint32_t)w, o[2] = (uint32_t)h, o[3] = (uint32_t)off;
+        break;
+      }
+      case RT_TEX_NOISE: {
+        int64_t pi = (int64_t)s[b + 2];
+        if (pi < 0 || (uint64_t)pi >= n_perl) {
+          *err = "noise texture perlin index out of range";
+          return RT_ERR_BAD_BLOB;
+        }
+        setd(o, 0, rd_f(b + 1)), o[1] = (uint32_t)pi;
+        break;
+      }
+      default:
+        *err = "unknown texture kind";
+        return RT_ERR_BAD_BLOB;
+    }
+  }
+  // checker cycles (the reference's Arc graph cannot form one; reject defensively)
+  for (uint64_t t = 0; t < n_tex; ++t) {
+    uint64_t id = t;
+    int steps = 0;
+    while (F.texs[id * RTL_TEX_WORDS] == RT_TEX_CHECKER && steps < 65) {
+      id = F.texs[id * RTL_TEX_WORDS + 1];
+      ++steps;
+    }
+    if (steps > 64) {
+      *err = "checker texture nesting deeper than 64";
+      return RT_ERR_UNSUPPORTED;
+    }
+  }
+  // materials
+  F.mats.assign(n_mat * RTL_MAT_WORDS, 0u);
+  bool pdf_mats = false, textured = false;
+  for (uint64_t m = 0; m < n_mat; ++m) {
+    uint64_t b = mat_off + m * RT_MAT_SLOTS;
+    uint32_t* o = &F.mats[m * RTL_MAT_WORDS];
+    int64_t kind = (int64_t)s[b];
+    switch (kind) {
+      case RT_MAT_LAMBERTIAN:
+      case RT_MAT_DIFFUSE_LIGHT:
+      case RT_MAT_ISOTROPIC: {
+        int64_t t = (int64_t)s[b + 1];
+        if (t < 0 || (uint64_t)t >= n_tex) {
+          *err = "material texture index out of range";
+          return RT_ERR_BAD_BLOB;
+        }
+        o[1] = (uint32_t)t;
+        o[0] = (uint32_t)kind | (tex_needs_uv(F.texs, (uint32_t)t, 0) ? RTL_MATF_NEEDS_UV : 0u);
+        if (kind != RT_MAT_DIFFUSE_LIGHT) pdf_mats = true;
+        if (F.texs[(size_t)t * RTL_TEX_WORDS] != RT_TEX_SOLID) textured = true;
+        break;
+      }
+      case RT_MAT_METAL:  // albedo3 fuzz
+        o[0] = (uint32_t)kind;
+        setd(o, 0, rd_f(b + 1)), setd(o, 1, rd_f(b + 2)), setd(o, 2, rd_f(b + 3));
+        setd(o, 3, rd_f(b + 4));
+        break;
+      case RT_MAT_DIELECTRIC:  // ir tint3
+        o[0] = (uint32_t)kind;
+        setd(o, 3, rd_f(b + 1));
+        setd(o, 0, rd_f(b + 2)), setd(o, 1, rd_f(b + 3)), setd(o, 2, rd_f(b + 4));
+        break;
+      default:
+        *err = "unknown material kind";
+        return RT_ERR_BAD_BLOB;
+    }
+  }
+  // perlin tables
+  F.perlin.assign(n_perl * RTL_PERLIN_BYTES, 0);
+  for (uint64_t p = 0; p < n_perl; ++p) {
+    uint64_t b = perl_off + p * RT_PERLIN_SLOTS;
+    double* rv = (double*)&F.perlin[p * RTL_PERLIN_BYTES];
+    for (int k = 0; k < 256; ++k) {
+      rv[4 * k] = rd_f(b + 3 * k);
+      rv[4 * k + 1] = rd_f(b + 3 * k + 1);
+      rv[4 * k + 2] = rd_f(b + 3 * k + 2);
+      rv[4 * k + 3] = 0.0;
+    }
+    uint8_t* perm = &F.perlin[p * RTL_PERLIN_BYTES + 8192];
+    for (int k = 0; k < 768; ++k) {
+      int64_t v = (int64_t)s[b + 768 + k];
+      if (v < 0 || v > 255) {
+        *err = "perlin permutation entry out of range";
+        return RT_ERR_BAD_BLOB;
+      }
+      perm[k] = (uint8_t)v;
+    }
+  }
+  // world
+  Reader r{s, n, world_off};
+  auto world = read_node(r, 0);
+  if (r.err || !world) {
+    *err = "world: " + r.msg;
+    return RT_ERR_BAD_BLOB;
+  }
+  if (world->tag != RT_OBJ_LIST) {
+    *err = "world must be a HittableList";
+    return RT_ERR_BAD_BLOB;
+  }
+  Emitter em(F.nodes, (int64_t)n_mat);
+  std::vector<uint32_t> chain;
+  em.emit(*world, -1, chain, false);
+  em.push(RTL_END, RTL_END_WORDS);
+  if (em.status != RT_OK) {
+    *err = em.err;
+    return em.status;
+  }
+  if (F.nodes.size() >= 0x7fffffffu) {
+    *err = "scene too large";
+    return RT_ERR_UNSUPPORTED;
+  }
+  // lights (HittablePDF over the lights object, pdf.rs:80-100)
+  uint32_t n_lights = 0, is_list = 0;
+  if (lights_off >= 0) {
+    Reader lr{s, n, (uint64_t)lights_off};
+    auto lights = lr.err ? nullptr : read_node(lr, 0);
+    if (lr.err || !lights) {
+      *err = "lights: " + lr.msg;
+      return RT_ERR_BAD_BLOB;
+    }
+    Emitter le(F.lights, (int64_t)n_mat);
+    auto one = [&](const Node& nd) {
+      F.light_offs.push_back((uint32_t)F.lights.size());
+      if (nd.tag == RT_OBJ_QUAD) le.quad(nd, true);
+      else if (nd.tag == RT_OBJ_SPHERE) le.sphere(nd, true);
+      else le.push(RTL_OTHER, 4);
+    };
+    if (lights->tag == RT_OBJ_LIST) {
+      is_list = 1;
+      for (auto& k : lights->kids) {
+        if (k->tag == RT_OBJ_LIST) {
+          *err = "nested HittableList inside the light list";
+          return RT_ERR_UNSUPPORTED;
+        }
+        one(*k);
+      }
+    } else {
+      one(*lights);
+    }
+    n_lights = (uint32_t)F.light_offs.size();
+    if (is_list && n_lights == 0) {
+      // An empty HittableList light object panics in the reference exactly like render_par.
+      is_list = 0;
+    }
+  }
+  if (blob->n_texels) F.texels.assign(blob->texels, blob->texels + blob->n_texels);
+  rtl_scene_header& h = F.hdr;
+  h.root = 0;
+  h.n_node_words = (uint32_t)F.nodes.size();
+  h.n_mats = (uint32_t)n_mat;
+  h.n_texs = (uint32_t)n_tex;
+  h.n_perlins = (uint32_t)n_perl;
+  h.n_lights = n_lights;
+  h.lights_is_list = is_list;
+  h.has_bvh = em.has_bvh;
+  h.has_volume = em.has_volume;
+  h.max_chain = em.max_chain;
+  h.n_texel_bytes = (uint32_t)n_texel;
+  h.pdf_materials = pdf_mats;
+  h.has_textures = textured;
+  return RT_OK;
+}
+
+}  // namespace rtf

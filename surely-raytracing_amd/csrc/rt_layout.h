@@ -1,0 +1,79 @@
+// rt_layout.h — device-resident scene layout (built by rt_flatten.cpp, read by rt_device.hip).
+//
+// The reference walks its object graph recursively (HittableList::hit hittable.rs:88-109,
+// BvhNode::hit :216-236, Translate/RotateY::hit transform.rs:57-135). On the GPU the graph is
+// flattened into ONE threaded pre-order word array: every node is followed in memory by its
+// first child, and carries a `skip` link to the first node after its subtree. Traversal is a
+// stack-free loop: "descend" = advance to the next node, "bbox miss" = follow skip. Visiting
+// order is exactly the reference's depth-first, left-then-right order, so the interval
+// shrinking (closest_so_far), tie behaviour and ConstantMedium RNG draw order are unchanged.
+//
+// Lists vanish (their children are simply consecutive). A Translate/RotateY node changes the
+// lane's local ray; an EXIT node after its subtree restores the parent frame by re-applying the
+// parent's transform chain to the world ray (same arithmetic as the recursive descent). The
+// boundary of a ConstantMedium is a sub-sequence terminated by END, traversed twice with its
+// own closest-hit state (constant_medium.rs:46-55).
+//
+// Word = 4 bytes; node offsets are word indices; every node starts 16-byte aligned.
+#pragma once
+#include <stdint.h>
+
+#define RTL_END 0
+#define RTL_QUAD 1
+#define RTL_SPHERE 2
+#define RTL_BVH 3
+#define RTL_TRANSLATE 4
+#define RTL_ROTATE_Y 5
+#define RTL_EXIT 6
+#define RTL_VOLUME 7
+#define RTL_OTHER 8 /* light entry whose pdf_value is 0 (Object default arm, object.rs:295-311) */
+/* header word 0: type | (flags << 8); word 1: skip (next node after the subtree).
+ * Payloads are f64 (the reference computes in f64) starting at word 4, read as
+ * 16-byte double2 pairs. dN = double index N counted from word 4. */
+/* QUAD (44 words): [hdr][skip][mat][0] d0-1 n.xy | d2-3 n.z,D | d4-5 q.xy | d6-7 q.z,area |
+ *   d8-9 w.xy | d10-11 w.z,0 | d12-13 u.xy | d14-15 u.z,0 | d16-17 v.xy | d18-19 v.z,0
+ *                                                                        object.rs:414-446 */
+#define RTL_QUAD_WORDS 44
+/* SPHERE (20 words): [hdr][skip][mat][moving] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r  object.rs:73-105 */
+#define RTL_SPHERE_WORDS 20
+/* BVH (16 words): [hdr][skip][0][0] d0-5 xmin xmax ymin ymax zmin zmax     hittable.rs:135-187 */
+#define RTL_BVH_WORDS 16
+/* TRANSLATE / ROTATE_Y (16 words):
+ *   [hdr][skip][chain_len][0] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
+ *   translate: p = offset.xyz; rotate_y: p0 = sin, p1 = cos                  transform.rs */
+#define RTL_XFORM_WORDS 16
+#define RTL_MAX_CHAIN 4
+/* EXIT (4 words): [hdr][skip=unused][parent frame node or -1][0] */
+#define RTL_EXIT_WORDS 4
+/* VOLUME (8 words): [hdr][skip][mat][0] d0 neg_inv_density, d1 0; the boundary follows and an
+ * END node terminates it                                                    constant_medium.rs */
+#define RTL_VOLUME_WORDS 8
+#define RTL_END_WORDS 4
+
+/* material (12 words): [kind | flags(bit8: texture reads uv)][tex][0][0] d0-3 c.xyz, param
+ *   METAL: c = albedo, param = fuzz; DIELECTRIC: c = tint, param = ir */
+#define RTL_MAT_WORDS 12
+#define RTL_MATF_NEEDS_UV 0x100u
+/* texture (12 words): [kind][a][b][c] d0-3
+ *   SOLID: d0-2 color; CHECKER: d0 inv_scale, a even, b odd;
+ *   IMAGE: a width, b height, c byte offset into texels; NOISE: d0 scale, a perlin index */
+#define RTL_TEX_WORDS 12
+/* perlin table: ranvec 256 x double4 (8192 B) + perm_x/y/z 3 x 256 bytes (768 B) */
+#define RTL_PERLIN_BYTES (8192 + 768)
+
+/* light entries: node-format QUAD / SPHERE / OTHER records in their own word array */
+typedef struct rtl_scene_header {
+  uint32_t root;          /* word offset of the world sequence                    */
+  uint32_t n_node_words;  /* nodes                                                */
+  uint32_t n_mats;
+  uint32_t n_texs;
+  uint32_t n_perlins;
+  uint32_t n_lights;      /* 0 = empty light list                                 */
+  uint32_t lights_is_list;/* 1: HittableList (random_int pick + 1/N average)      */
+  uint32_t has_bvh;
+  uint32_t has_volume;
+  uint32_t max_chain;
+  uint32_t n_texel_bytes;
+  uint32_t pdf_materials; /* any Lambertian / Isotropic                           */
+  uint32_t has_textures;  /* a material references a non-solid texture            */
+} rtl_scene_header;

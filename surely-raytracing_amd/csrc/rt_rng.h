@@ -1,0 +1,57 @@
+// rt_rng.h — counter-keyed per-sample RNG of the device path.
+//
+// The reference draws every random number from rand::thread_rng (ChaCha12, OS-seeded,
+// utils.rs:5-15), so it is unseeded and its draw order depends on rayon scheduling. Here each
+// pixel-sample owns an independent stream keyed by (seed, global pixel index, sample index):
+// pcg4d (Jarzynski & Olano 2020) hashes the key into the state of xoshiro128**; draws are then
+// consumed in exactly the reference's call order. Results are reproducible and independent of
+// how pixels are distributed over lanes, waves or GPUs. The CPU oracle implements the same
+// generator (oracle/rt_oracle.c).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+struct Rng {
+  uint32_t s0, s1, s2, s3;
+};
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+__device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel,
+                                        uint32_t sample) {
+  uint32_t v0 = pixel * 1664525u + 1013904223u, v1 = sample * 1664525u + 1013904223u;
+  uint32_t v2 = seed_lo * 1664525u + 1013904223u, v3 = seed_hi * 1664525u + 1013904223u;
+  v0 += v1 * v3;
+  v1 += v2 * v0;
+  v2 += v0 * v1;
+  v3 += v1 * v2;
+  v0 ^= v0 >> 16;
+  v1 ^= v1 >> 16;
+  v2 ^= v2 >> 16;
+  v3 ^= v3 >> 16;
+  v0 += v1 * v3;
+  v1 += v2 * v0;
+  v2 += v0 * v1;
+  v3 += v1 * v2;
+  if ((v0 | v1 | v2 | v3) == 0u) v0 = 0x9E3779B9u;
+  return {v0, v1, v2, v3};
+}
+__device__ __forceinline__ uint32_t rng_u32(Rng& g) {
+  uint32_t result = rotl32(g.s1 * 5u, 7) * 9u;
+  uint32_t t = g.s1 << 9;
+  g.s2 ^= g.s0;
+  g.s3 ^= g.s1;
+  g.s1 ^= g.s2;
+  g.s0 ^= g.s3;
+  g.s2 ^= t;
+  g.s3 = rotl32(g.s3, 11);
+  return result;
+}
+// random_double (utils.rs:5-7): 32-bit uniform in [0, 1), exact in f64
+__device__ __forceinline__ double rnd(Rng& g) { return (double)rng_u32(g) * 0x1p-32; }
+// random_range(-1, 1) (utils.rs:9-11)
+__device__ __forceinline__ double rnd_pm1(Rng& g) { return -1.0 + 2.0 * rnd(g); }
+// random_int(0, n-1) (utils.rs:13-15): multiply-high
+__device__ __forceinline__ uint32_t rnd_index(Rng& g, uint32_t n) { return __umulhi(rng_u32(g), n); }
+
+}  // namespace rtd
