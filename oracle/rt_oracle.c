@@ -1162,10 +1162,74 @@ EXPORT int oracle_render(const rt_scene_blob* blob, const rt_camera* cam, const 
 }
 
 /* ---- unit entry points for known-answer tests ------------------------------------------ */
-EXPORT void oracle_rng_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int n, float* out) {
+EXPORT void oracle_rng_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int n, double* out) {
   rng_t g;
   rng_seed(&g, seed, pixel, sample);
-  for (int i = 0; i < n; ++i) out[i] = (float)rnd(&g);
+  for (int i = 0; i < n; ++i) out[i] = (double)rnd(&g);
+}
+EXPORT void oracle_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, int n, uint32_t* out) {
+  rng_t g;
+  rng_seed(&g, seed, pixel, sample);
+  for (int i = 0; i < n; ++i) out[i] = rng_u32(&g);
+}
+/* get_sphere_uv (object.rs:114-120) at unit-sphere points p[3*i..] -> uv[2*i..] */
+EXPORT void oracle_sphere_uv(const double* p, int n, double* uv) {
+  for (int i = 0; i < n; ++i) {
+    real u, v;
+    sphere_uv(v3(R(p[3 * i]), R(p[3 * i + 1]), R(p[3 * i + 2])), &u, &v);
+    uv[2 * i] = (double)u;
+    uv[2 * i + 1] = (double)v;
+  }
+}
+/* HittablePDF::value of the scene's light object at `origin` for n directions. */
+EXPORT int oracle_light_pdf_batch(const rt_scene_blob* blob, const double* origin3, const double* dirs,
+                                  int n, double* out) {
+  oscene sc;
+  if (parse_scene(blob, &sc)) return -1;
+  if (sc.lights < 0) {
+    free_scene(&sc);
+    return -2;
+  }
+  ctx_t cx;
+  memset(&cx, 0, sizeof(cx));
+  cx.sc = &sc;
+  vec3 o = v3(R(origin3[0]), R(origin3[1]), R(origin3[2]));
+  for (int i = 0; i < n; ++i)
+    out[i] = (double)light_pdf_value(&cx, sc.lights, o, v3(R(dirs[3 * i]), R(dirs[3 * i + 1]), R(dirs[3 * i + 2])));
+  free_scene(&sc);
+  return 0;
+}
+/* n light-PDF generate() draws at `origin` with the stream of (seed, 0, k): dirs[3*k..] */
+EXPORT int oracle_light_generate(const rt_scene_blob* blob, const double* origin3, uint64_t seed, int n,
+                                 double* dirs) {
+  oscene sc;
+  if (parse_scene(blob, &sc)) return -1;
+  if (sc.lights < 0) {
+    free_scene(&sc);
+    return -2;
+  }
+  ctx_t cx;
+  memset(&cx, 0, sizeof(cx));
+  cx.sc = &sc;
+  vec3 o = v3(R(origin3[0]), R(origin3[1]), R(origin3[2]));
+  for (int k = 0; k < n; ++k) {
+    rng_t g;
+    rng_seed(&g, seed, 0, (uint32_t)k);
+    vec3 d = light_random(&cx, sc.lights, o, &g);
+    dirs[3 * k] = d.x, dirs[3 * k + 1] = d.y, dirs[3 * k + 2] = d.z;
+  }
+  free_scene(&sc);
+  return 0;
+}
+/* n cosine-PDF directions about unit normal w (onb.rs + vec3.rs:240-250) */
+EXPORT void oracle_cosine_dirs(const double* w3, uint64_t seed, int n, double* dirs) {
+  onb_t b = onb_from_w(v3(R(w3[0]), R(w3[1]), R(w3[2])));
+  for (int k = 0; k < n; ++k) {
+    rng_t g;
+    rng_seed(&g, seed, 1, (uint32_t)k);
+    vec3 d = onb_local(&b, random_cosine_direction(&g));
+    dirs[3 * k] = d.x, dirs[3 * k + 1] = d.y, dirs[3 * k + 2] = d.z;
+  }
 }
 EXPORT void oracle_fmath(int fn, const float* x, const float* y, int n, float* out) {
   for (int i = 0; i < n; ++i) {

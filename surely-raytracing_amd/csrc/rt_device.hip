@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -131,20 +132,35 @@ struct TraceParams {
   int tiles_x;
 };
 
-// ---------------------------------------------------------------- loads (16 B, dwordx4)
-__device__ __forceinline__ double2 ldd2(const uint32_t* p) {
-  return *reinterpret_cast<const double2*>(p);
-}
-// xyz of the f64 triple starting at double index k of a node (payload begins at word 4)
-__device__ __forceinline__ d3 ld3(const uint32_t* X, int k) {
+// ---------------------------------------------------------------- loads
+// Two pointer kinds reach the same node records:
+//  gptr: per-lane (divergent) node index -> vector loads (global_load_dwordx4 through L1/L2)
+//  kptr: wave-uniform node index (no BVH: every lane walks the same node sequence) -> the
+//        constant address space lets hipcc use scalar loads (s_load_dwordx*, K$), so node
+//        data lands in SGPRs and costs neither VGPRs nor vector-memory latency.
+typedef const uint32_t* gptr;
+typedef const __attribute__((address_space(4))) uint32_t* kptr;
+typedef const __attribute__((address_space(4))) double* kdptr;
+
+__device__ __forceinline__ d3 ld3(gptr X, int k) {  // f64 triple at payload double index k
   const double* d = reinterpret_cast<const double*>(X + 4) + k;
-  double2 a = *reinterpret_cast<const double2*>(d);
-  return mk(a.x, a.y, d[2]);
+  if ((k & 1) == 0) {
+    double2 a = *reinterpret_cast<const double2*>(d);
+    return mk(a.x, a.y, d[2]);
+  }
+  double2 b = *reinterpret_cast<const double2*>(d + 1);
+  return mk(d[0], b.x, b.y);
 }
-__device__ __forceinline__ double ldd(const uint32_t* X, int k) {
+__device__ __forceinline__ d3 ld3(kptr X, int k) {
+  kdptr d = reinterpret_cast<kdptr>(X + 4) + k;
+  return mk(d[0], d[1], d[2]);
+}
+__device__ __forceinline__ double ldd(gptr X, int k) {
   return reinterpret_cast<const double*>(X + 4)[k];
 }
-__device__ __forceinline__ uint4 ld4u(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ double ldd(kptr X, int k) { return reinterpret_cast<kdptr>(X + 4)[k]; }
+__device__ __forceinline__ uint4 ld4u(gptr p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint4 ld4u(kptr p) { return make_uint4(p[0], p[1], p[2], p[3]); }
 __device__ __forceinline__ d3 arr3(const double* a) { return mk(a[0], a[1], a[2]); }
 
 // ---------------------------------------------------------------- op counters (COUNT build)
@@ -170,16 +186,15 @@ struct Ctr<true> {
 
 // ---------------------------------------------------------------- primitives
 // Quad::hit object.rs:453-490; inclusive interval (Interval::contains interval.rs:21-23).
-template <bool COUNT>
-__device__ __forceinline__ bool quad_test(const uint32_t* q, d3 o, d3 d, double tmin, double tmax,
+template <bool COUNT, class Ptr>
+__device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double tmax,
                                           double& t_out, Ctr<COUNT>& C) {
   C.inc(RT_OP_QUAD_TESTS);
-  double2 n01 = ldd2(q + 4), n2D = ldd2(q + 8);
-  d3 n = mk(n01.x, n01.y, n2D.x);
+  d3 n = ld3(q, 0);
   double denom = dot(n, d);
   if (fabs(denom) < 1e-8) return false;
   C.inc(RT_OP_QUAD_PLANE);
-  double t = (n2D.y - dot(n, o)) / denom;
+  double t = (ldd(q, 3) - dot(n, o)) / denom;
   if (!(tmin <= t && t <= tmax)) return false;
   C.inc(RT_OP_QUAD_INTERVAL);
   d3 p = vfma(t, d, o);
@@ -194,17 +209,17 @@ __device__ __forceinline__ bool quad_test(const uint32_t* q, d3 o, d3 d, double 
 }
 
 // Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
-template <bool COUNT>
-__device__ __forceinline__ bool sphere_test(const uint32_t* s, d3 o, d3 d, double tm, double tmin,
+template <bool COUNT, class Ptr>
+__device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double tmin,
                                             double tmax, double& t_out, Ctr<COUNT>& C) {
   C.inc(RT_OP_SPHERE_TESTS);
-  double2 c01 = ldd2(s + 4), c2r = ldd2(s + 8);
-  d3 center = mk(c01.x, c01.y, c2r.x);
+  d3 center = ld3(s, 0);
+  double r = ldd(s, 3);
   if (s[3]) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
   d3 oc = o - center;
   double a = dot(d, d);
   double half_b = dot(oc, d);
-  double c = dot(oc, oc) - c2r.y * c2r.y;
+  double c = dot(oc, oc) - r * r;
   double disc = fma(half_b, half_b, -(a * c));
   if (disc < 0.0) return false;
   C.inc(RT_OP_SPHERE_ROOTS);
@@ -220,10 +235,10 @@ __device__ __forceinline__ bool sphere_test(const uint32_t* s, d3 o, d3 d, doubl
 }
 
 // Aabb::hit object.rs:340-370 with inv_d = 1/d computed once per ray frame.
-__device__ __forceinline__ bool aabb_test(const uint32_t* b, d3 o, d3 inv, double tmin,
-                                          double tmax) {
-  double2 bx = ldd2(b + 4), by = ldd2(b + 8), bz = ldd2(b + 12);
-  const double mn[3] = {bx.x, by.x, bz.x}, mx[3] = {bx.y, by.y, bz.y};
+template <class Ptr>
+__device__ __forceinline__ bool aabb_test(Ptr b, d3 o, d3 inv, double tmin, double tmax) {
+  const double mn[3] = {ldd(b, 0), ldd(b, 2), ldd(b, 4)};
+  const double mx[3] = {ldd(b, 1), ldd(b, 3), ldd(b, 5)};
   const double oo[3] = {o.x, o.y, o.z}, id[3] = {inv.x, inv.y, inv.z};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -242,30 +257,29 @@ __device__ __forceinline__ bool aabb_test(const uint32_t* b, d3 o, d3 inv, doubl
 }
 
 // Translate/RotateY ray into object space (transform.rs:59, 86-107).
-__device__ __forceinline__ void xform_in(const uint32_t* X, d3& o, d3& d) {
-  double2 p01 = ldd2(X + 8);
+template <class Ptr>
+__device__ __forceinline__ void xform_in(Ptr X, d3& o, d3& d) {
   if ((X[0] & 0xffu) == RTL_TRANSLATE) {
-    o = o - mk(p01.x, p01.y, ldd(X, 4));
+    o = o - ld3(X, 2);
   } else {
-    double s = p01.x, c = p01.y;
+    double s = ldd(X, 2), c = ldd(X, 3);
     o = mk(fma(c, o.x, -(s * o.z)), o.y, fma(s, o.x, c * o.z));
     d = mk(fma(c, d.x, -(s * d.z)), d.y, fma(s, d.x, c * d.z));
   }
 }
 // Hit record back to the parent space (transform.rs:65, 114-130).
-__device__ __forceinline__ void xform_out(const uint32_t* X, d3& p, d3& n) {
-  double2 p01 = ldd2(X + 8);
+__device__ __forceinline__ void xform_out(gptr X, d3& p, d3& n) {
   if ((X[0] & 0xffu) == RTL_TRANSLATE) {
-    p = p + mk(p01.x, p01.y, ldd(X, 4));
+    p = p + ld3(X, 2);
   } else {
-    double s = p01.x, c = p01.y;
+    double s = ldd(X, 2), c = ldd(X, 3);
     p = mk(fma(c, p.x, s * p.z), p.y, fma(-s, p.x, c * p.z));
     n = mk(fma(c, n.x, s * n.z), n.y, fma(-s, n.x, c * n.z));
   }
 }
 // Local ray of `frame` = the world ray pushed through its transform chain, root first.
-__device__ __forceinline__ void frame_ray(const uint32_t* __restrict__ N, int frame, d3 wo, d3 wd,
-                                          d3& o, d3& d) {
+template <class Ptr>
+__device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o, d3& d) {
   o = wo;
   d = wd;
   if (frame < 0) return;
@@ -280,17 +294,24 @@ __device__ __forceinline__ void frame_ray(const uint32_t* __restrict__ N, int fr
 // ---------------------------------------------------------------- traversal
 // Threaded walk of the flattened scene (rt_layout.h). MAIN: the world (records the hit node and
 // its frame, handles ConstantMedium when VOL). !MAIN: a volume boundary (closest t only).
-template <bool MAIN, bool COUNT, bool VOL>
+// UNI: the scene has no BVH, so the node sequence is the same for every lane and the node
+// index is kept wave-uniform (scalar loads). Otherwise each lane follows its own skips.
+template <bool MAIN, bool COUNT, bool VOL, bool UNI>
 __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, double tm, d3 o, d3 d,
                          int frame, double tmin, double tmax, double& t_out, uint32_t& hit_node,
                          int& hit_frame, Rng& g, Ctr<COUNT>& C) {
-  const uint32_t* __restrict__ N = P.nodes;
+  typedef typename std::conditional<UNI, kptr, gptr>::type Ptr;
+  const Ptr N = (Ptr)P.nodes;
   double closest = tmax;
   bool hit = false;
   d3 inv = mk(0., 0., 0.);
   bool inv_ok = false;
   for (;;) {
-    const uint32_t* X = N + node;
+    if (UNI) {
+      node = __builtin_amdgcn_readfirstlane(node);
+      frame = __builtin_amdgcn_readfirstlane(frame);
+    }
+    const Ptr X = N + node;
     uint4 h = ld4u(X);
     uint32_t type = h.x & 0xffu;
     if (type == RTL_QUAD) {
@@ -339,9 +360,9 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
       double t1, t2;
       uint32_t dn;
       int df;
-      if (traverse<false, COUNT, false>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
+      if (traverse<false, COUNT, false, UNI>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
                                         -INFINITY, INFINITY, t1, dn, df, g, C) &&
-          traverse<false, COUNT, false>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
+          traverse<false, COUNT, false, UNI>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
                                         t1 + 0.0001, INFINITY, t2, dn, df, g, C)) {
         if (t1 < tmin) t1 = tmin;
         if (t2 > closest) t2 = closest;
@@ -514,7 +535,7 @@ template <bool COUNT>
 __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>& C) {
   double sum = 0.0;
   for (uint32_t i = 0; i < P.n_lights; ++i) {
-    const uint32_t* L = P.lights + P.light_offs[i];
+    const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
     uint32_t type = L[0] & 0xffu;
     double pv = 0.0;
     if (type == RTL_QUAD) {
@@ -573,7 +594,7 @@ __device__ d3 light_random(const TraceParams& P, d3 origin, Rng& g) {
 
 // ---------------------------------------------------------------- the path kernel
 // VOL: scene has ConstantMedium nodes; TEX: some material reads a non-solid texture.
-template <bool COUNT, bool VOL, bool TEX>
+template <bool COUNT, bool VOL, bool TEX, bool UNI>
 __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
   __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
   if (COUNT) {
@@ -643,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
     double t;
     uint32_t hn = 0;
     int hf = -1;
-    if (!traverse<true, COUNT, VOL>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
+    if (!traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
                                     hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * arr3(P.bg);
@@ -994,10 +1015,19 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
   const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
-  auto kern = count ? (vol ? (tex ? rt_trace<true, true, true> : rt_trace<true, true, false>)
-                           : (tex ? rt_trace<true, false, true> : rt_trace<true, false, false>))
-                    : (vol ? (tex ? rt_trace<false, true, true> : rt_trace<false, true, false>)
-                           : (tex ? rt_trace<false, false, true> : rt_trace<false, false, false>));
+  const bool uni = sc->hdr.has_bvh == 0;
+  typedef void (*kern_t)(TraceParams);
+  // [count][vol][tex][uni]
+  static const kern_t table[16] = {
+      rt_trace<false, false, false, false>, rt_trace<false, false, false, true>,
+      rt_trace<false, false, true, false>,  rt_trace<false, false, true, true>,
+      rt_trace<false, true, false, false>,  rt_trace<false, true, false, true>,
+      rt_trace<false, true, true, false>,   rt_trace<false, true, true, true>,
+      rt_trace<true, false, false, false>,  rt_trace<true, false, false, true>,
+      rt_trace<true, false, true, false>,   rt_trace<true, false, true, true>,
+      rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
+      rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
+  kern_t kern = table[(count ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) + (uni ? 1 : 0)];
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
   HIP_TRY(hipGetLastError());
   if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));

@@ -158,35 +158,39 @@ def device_lib() -> C.CDLL:
     """The product library. Raises if it is not built: there is no CPU fallback."""
     global _dev
     if _dev is None:
-        path = BUILD / "librtmi355x.so"
-        if not path.exists():
-            raise RuntimeError(f"{path} missing: the HIP library is required (run `make device`)")
-        lib = C.CDLL(str(path))
-        p = C.c_void_p
-        sig = {
-            "rt_abi_version": (C.c_int, []),
-            "rt_last_error": (C.c_char_p, []),
-            "rt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
-            "rt_scene_validate": (C.c_int, [C.POINTER(RtSceneBlob)]),
-            "rt_scene_create": (C.c_int, [C.POINTER(RtSceneBlob), C.c_int, C.POINTER(p)]),
-            "rt_scene_destroy": (None, [p]),
-            "rt_scene_device_bytes": (C.c_uint64, [p]),
-            "rt_render": (C.c_int, [p, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
-                                    C.POINTER(RtStats)]),
-            "rt_render_device": (C.c_int, [p, C.POINTER(RtCamera), C.POINTER(RtRenderOpts),
-                                           C.c_void_p, C.c_void_p, C.POINTER(RtStats)]),
-            "rt_render_blob": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
-                                         C.POINTER(RtRenderOpts), C.c_void_p,
-                                         C.POINTER(RtStats)]),
-        }
-        for name, (res, args) in sig.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        if lib.rt_abi_version() != 1:
-            raise RuntimeError("librtmi355x ABI version mismatch")
-        _dev = lib
+        _dev = load_device_lib(BUILD / "librtmi355x.so")
     return _dev
+
+
+def load_device_lib(path: Path) -> C.CDLL:
+    path = Path(path)
+    if not path.exists():
+        raise RuntimeError(f"{path} missing: the HIP library is required (run `make device`)")
+    lib = C.CDLL(str(path))
+    p = C.c_void_p
+    sig = {
+        "rt_abi_version": (C.c_int, []),
+        "rt_last_error": (C.c_char_p, []),
+        "rt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "rt_scene_validate": (C.c_int, [C.POINTER(RtSceneBlob)]),
+        "rt_scene_create": (C.c_int, [C.POINTER(RtSceneBlob), C.c_int, C.POINTER(p)]),
+        "rt_scene_destroy": (None, [p]),
+        "rt_scene_device_bytes": (C.c_uint64, [p]),
+        "rt_render": (C.c_int, [p, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
+                                C.POINTER(RtStats)]),
+        "rt_render_device": (C.c_int, [p, C.POINTER(RtCamera), C.POINTER(RtRenderOpts),
+                                       C.c_void_p, C.c_void_p, C.POINTER(RtStats)]),
+        "rt_render_blob": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
+                                     C.POINTER(RtRenderOpts), C.c_void_p,
+                                     C.POINTER(RtStats)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rt_abi_version() != 1:
+        raise RuntimeError("librtmi355x ABI version mismatch")
+    return lib
 
 
 def _check_host(rc: int) -> int:

@@ -32,6 +32,15 @@ def lib(precision: int = 32) -> C.CDLL:
         L.oracle_render.argtypes = [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
                                     C.POINTER(RtRenderOpts), C.c_void_p, C.c_void_p, C.c_int]
         L.oracle_rng_draws.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
+        L.oracle_rng_u32.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
+        L.oracle_sphere_uv.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_light_pdf_batch.restype = C.c_int
+        L.oracle_light_pdf_batch.argtypes = [C.POINTER(RtSceneBlob), C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_void_p]
+        L.oracle_light_generate.restype = C.c_int
+        L.oracle_light_generate.argtypes = [C.POINTER(RtSceneBlob), C.c_void_p, C.c_uint64, C.c_int,
+                                            C.c_void_p]
+        L.oracle_cosine_dirs.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
         L.oracle_fmath.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_camera_ray.argtypes = [C.POINTER(RtCamera), C.c_uint64, C.c_int, C.c_int,
                                         C.c_int, C.c_int, C.c_void_p]
@@ -46,7 +55,7 @@ def lib(precision: int = 32) -> C.CDLL:
     return _libs[precision]
 
 
-def render(blob, cam: RtCamera, opts: RtRenderOpts, precision: int = 32, threads: int | None = None,
+def render(blob, cam: RtCamera, opts: RtRenderOpts, precision: int = 64, threads: int | None = None,
            accum: np.ndarray | None = None):
     """oracle_render -> (accum float32 [n_rows, W, 3], op-count dict)."""
     if threads is None:
@@ -62,9 +71,50 @@ def render(blob, cam: RtCamera, opts: RtRenderOpts, precision: int = 32, threads
     return accum, {n: int(ops[i]) for i, n in enumerate(OP_NAMES)}
 
 
-def rng_draws(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
-    out = np.zeros(n, np.float32)
-    lib(32).oracle_rng_draws(seed, pixel, sample, n, out.ctypes.data)
+def rng_draws(seed: int, pixel: int, sample: int, n: int, precision: int = 64) -> np.ndarray:
+    """random_double() stream of one pixel-sample (f64 build: 32-bit uniforms)."""
+    out = np.zeros(n, np.float64)
+    lib(precision).oracle_rng_draws(seed, pixel, sample, n, out.ctypes.data)
+    return out
+
+
+def rng_u32(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.uint32)
+    lib(64).oracle_rng_u32(seed, pixel, sample, n, out.ctypes.data)
+    return out
+
+
+def sphere_uv(points: np.ndarray, precision: int = 64) -> np.ndarray:
+    p = np.ascontiguousarray(points, np.float64).reshape(-1, 3)
+    out = np.zeros((p.shape[0], 2), np.float64)
+    lib(precision).oracle_sphere_uv(p.ctypes.data, p.shape[0], out.ctypes.data)
+    return out
+
+
+def light_pdf_batch(blob, origin, dirs, precision: int = 64) -> np.ndarray:
+    o = np.ascontiguousarray(origin, np.float64)
+    d = np.ascontiguousarray(dirs, np.float64).reshape(-1, 3)
+    out = np.zeros(d.shape[0], np.float64)
+    rc = lib(precision).oracle_light_pdf_batch(blob.ref(), o.ctypes.data, d.ctypes.data, d.shape[0],
+                                               out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"oracle_light_pdf_batch: {rc}")
+    return out
+
+
+def light_generate(blob, origin, n, seed=1, precision: int = 64) -> np.ndarray:
+    o = np.ascontiguousarray(origin, np.float64)
+    out = np.zeros((n, 3), np.float64)
+    rc = lib(precision).oracle_light_generate(blob.ref(), o.ctypes.data, seed, n, out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"oracle_light_generate: {rc}")
+    return out
+
+
+def cosine_dirs(w, n, seed=1, precision: int = 64) -> np.ndarray:
+    ww = np.ascontiguousarray(w, np.float64)
+    out = np.zeros((n, 3), np.float64)
+    lib(precision).oracle_cosine_dirs(ww.ctypes.data, seed, n, out.ctypes.data)
     return out
 
 
@@ -80,13 +130,13 @@ def fmath(fn: str, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:
 
 
 def camera_ray(cam: RtCamera, seed: int, i: int, j: int, s_i: int, s_j: int,
-               precision: int = 32) -> np.ndarray:
+               precision: int = 64) -> np.ndarray:
     out = np.zeros(7, np.float64)
     lib(precision).oracle_camera_ray(C.byref(cam), seed, i, j, s_i, s_j, out.ctypes.data)
     return out
 
 
-def world_hit(blob, ray7, tmin=1e-4, tmax=float("inf"), precision: int = 32):
+def world_hit(blob, ray7, tmin=1e-4, tmax=float("inf"), precision: int = 64):
     r = np.ascontiguousarray(ray7, np.float64)
     out = np.zeros(9, np.float64)
     h = lib(precision).oracle_world_hit(blob.ref(), r.ctypes.data, tmin, tmax, out.ctypes.data)
@@ -95,7 +145,7 @@ def world_hit(blob, ray7, tmin=1e-4, tmax=float("inf"), precision: int = 32):
     return out if h else None
 
 
-def light_pdf(blob, origin, direction, precision: int = 32) -> float:
+def light_pdf(blob, origin, direction, precision: int = 64) -> float:
     o = np.ascontiguousarray(origin, np.float64)
     d = np.ascontiguousarray(direction, np.float64)
     out = C.c_double()

@@ -1,0 +1,90 @@
+"""The C-ABI libraries load and export every symbol their headers declare; blob validation
+(host-only, no GPU) accepts reference scenes and rejects malformed ones with a status code."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import surely_rt as rt
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _declared(header: str):
+    text = (REPO / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b((?:rt|rth)_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.mark.parametrize("header,lib", [("rt_mi355x.h", "librtmi355x.so"),
+                                        ("rt_host.h", "librthost.so")])
+def test_exports_every_declared_symbol(header, lib):
+    names = _declared(header)
+    assert len(names) >= 8
+    so = C.CDLL(str(REPO / "build" / lib))
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_error_string():
+    lib = rt.device_lib()
+    assert lib.rt_abi_version() == 1
+    assert isinstance(lib.rt_last_error(), bytes)
+
+
+def test_validate_accepts_all_presets():
+    lib = rt.device_lib()
+    for name in ["cornell_box", "cornell_smoke", "final_scene", "quads", "simple_light",
+                 "two_spheres", "two_perlin_spheres", "random_balls", "three_spheres", "earth"]:
+        blob, cam = rt.preset_blob(name, width=32, spp=4)
+        assert lib.rt_scene_validate(blob.ref()) == rt.RT_OK, (name, lib.rt_last_error())
+
+
+def test_validate_rejects_malformed_blobs():
+    lib = rt.device_lib()
+    blob, _ = rt.preset_blob("cornell_box", width=32, spp=4)
+    bad = blob.slots.copy()
+    bad[0] = 0  # magic
+    assert lib.rt_scene_validate(rt.Blob(bad, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
+    bad = blob.slots.copy()
+    bad[2] = bad[2] + 1  # size mismatch
+    assert lib.rt_scene_validate(rt.Blob(bad, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
+    bad = blob.slots[: int(blob.slots[9]) + 3].copy()  # truncated world tree
+    bad[2] = bad.size
+    assert lib.rt_scene_validate(rt.Blob(bad, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
+    bad = blob.slots.copy()
+    w = int(bad[9])
+    bad[w] = 99  # unknown object tag
+    assert lib.rt_scene_validate(rt.Blob(bad, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
+    assert "tag" in lib.rt_last_error().decode()
+
+
+def test_validate_rejects_out_of_range_material():
+    sc = rt.Scene(1)
+    m = sc.lambertian((0.5, 0.5, 0.5))
+    world = sc.hittable_list(sc.sphere((0, 0, 0), 1, m))
+    blob = sc.serialize(world)
+    slots = blob.slots.copy()
+    w = int(slots[9])
+    # LIST [tag n bbox6] then SPHERE [tag mat ...]
+    slots[w + 8 + 1] = 1000
+    lib = rt.device_lib()
+    assert lib.rt_scene_validate(rt.Blob(slots, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
+
+
+def test_unsupported_nesting_reported():
+    """A ConstantMedium whose boundary contains another ConstantMedium is valid Rust but the
+    device traversal keeps one boundary sub-walk: rejected with RT_ERR_UNSUPPORTED."""
+    sc = rt.Scene(1)
+    inner = sc.constant_medium(sc.sphere((0, 0, 0), 1, sc.dielectric(1.5)), 0.5, (1, 1, 1))
+    outer = sc.constant_medium(sc.hittable_list(inner), 0.5, (1, 1, 1))
+    blob = sc.serialize(sc.hittable_list(outer))
+    assert rt.device_lib().rt_scene_validate(blob.ref()) == rt.RT_ERR_UNSUPPORTED
+
+
+def test_product_path_fails_loudly_without_library(tmp_path):
+    """No CPU fallback: with the HIP library absent, loading the render path raises."""
+    with pytest.raises(RuntimeError, match="HIP library is required"):
+        rt.load_device_lib(tmp_path / "librtmi355x.so")

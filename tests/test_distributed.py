@@ -1,0 +1,85 @@
+"""The multi-rank row tiling + gather path (surely_rt.parallel) on CPU with gloo, world_size 2
+and 3. Each rank renders its cyclic rows and the frame is gathered to rank 0, which must equal
+a single-process render bitwise. The per-rank renderer here is the CPU oracle standing in for
+the GPU (test infrastructure); bench.py drives the same helpers with the HIP library + RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo / "surely-raytracing_amd"))
+    sys.path.insert(0, str(repo / "tests"))
+    import oracle_lib as O
+    import surely_rt as rt
+    from surely_rt.parallel import cyclic_rows, gather_frame, max_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob, cam = rt.preset_blob("cornell_box", width=37, spp=4)
+        H, W = cam.image_height, cam.image_width
+        b, s, n = cyclic_rows(H, rank, world)
+        part, _ = O.render(blob, cam, rt.make_opts(cam, seed=3, row_begin=b, row_step=s, n_rows=n),
+                           threads=1)
+        local = torch.zeros((max_rows(H, world), W, 3), dtype=torch.float32)
+        local[:n] = torch.from_numpy(part)
+        frame = gather_frame(local, H, rank, world)
+        if rank == 0:
+            full, _ = O.render(blob, cam, rt.make_opts(cam, seed=3), threads=2)
+            q.put(bool(np.array_equal(frame.numpy(), full)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_tiling_gather_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_cyclic_rows_partition():
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "surely-raytracing_amd"))
+    from surely_rt.parallel import cyclic_rows, deinterleave, max_rows
+
+    for H in (1, 7, 800, 2160):
+        for world in (1, 2, 3, 8):
+            rows = []
+            for r in range(world):
+                b, s, n = cyclic_rows(H, r, world)
+                rows += list(range(b, H, s))[:n]
+                assert n <= max_rows(H, world)
+            assert sorted(rows) == list(range(H))
+    g = np.arange(2 * 3 * 1 * 3, dtype=np.float32).reshape(2, 3, 1, 3)
+    out = deinterleave(g, 5, 2)
+    assert np.array_equal(out[0], g[0, 0]) and np.array_equal(out[1], g[1, 0])
+    assert np.array_equal(out[4], g[0, 2])
