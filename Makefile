@@ -46,3 +46,11 @@ oracle/_build/liboracle_f64.so: oracle/rt_oracle.c include/rt_mi355x.h
 
 clean:
 	rm -rf $(BUILD) oracle/_build
+
+# performance variants for A/B measurement (tools_gpu/ab_variants.py); not shipped
+VARIANTS := $(BUILD)/variants
+variants: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(VARIANTS)
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=1 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w1.so
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=3 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w3.so
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=4 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w4.so

@@ -7,17 +7,21 @@
 // Material scatter (material.rs:92-248), PDFs (pdf.rs:44-127), Onb (onb.rs:24-47), textures
 // and Perlin noise (texture.rs:17-131, perlin.rs:30-96), vec3 math (vec3.rs).
 //
-// Work decomposition: one lane = one (pixel, stratum row s_j); the lane walks
-// the sqrt_spp samples s_i of that row, regenerating a camera path as soon as the previous one
-// terminates (ray_color's recursion -> an iterative bounce loop with beta/L), so lanes of a
-// wave stay busy while path lengths differ. A wave = an 8x8 pixel tile at one s_j; the tile's
-// rows are adjacent, so camera rays and first hits are coherent. Row sums go to a per-(s_j,
-// pixel) partial buffer; rt_reduce sums them in s_j order into the caller's accumulator.
-// No atomics touch the framebuffer: the sum order is fixed, so results are bitwise
-// reproducible and identical across 1..8 GPUs (the RNG is keyed by global pixel and sample).
+// Work decomposition: a wave owns a POOL = one 8x8 pixel tile x one stratum row
+// s_j x all sqrt_spp samples s_i of that row (64 x 31 paths for 961 spp). Each lane traces one
+// path at a time (ray_color's recursion -> an iterative bounce loop with beta/L); when it
+// terminates, the lane stores the sample's radiance and claims the next pool item with a wave
+// ballot + mbcnt, so lanes stay busy until the pool drains whatever the per-pixel path cost.
+// The first 64 items are s_i = 0 for every pixel of the tile: camera rays and first hits are
+// coherent. Samples land in a per-sample slot; rt_reduce sums them in the reference's order
+// (s_i inside s_j, render.rs:185-189) into the caller's accumulator, so no atomics touch the
+// framebuffer and results are bitwise reproducible and identical across 1..8 GPUs (the RNG is
+// keyed by global pixel and sample).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <type_traits>
 #include <cstdio>
 #include <cstring>
@@ -41,6 +45,11 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 constexpr int kBlock = 256;   // 4 waves per workgroup
+// Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument): 4 caps the
+// allocation at 128 VGPRs (tools_gpu/ab_variants.py measures the trade against spills).
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 4
+#endif
 
 struct d3 {
   double x, y, z;
@@ -66,9 +75,30 @@ __device__ __forceinline__ d3 vfma(double t, d3 a, d3 b) {  // t*a + b
 __device__ __forceinline__ d3 cross(d3 u, d3 v) {  // vec3.rs:171-177
   return {fma(u.y, v.z, -(u.z * v.y)), fma(u.z, v.x, -(u.x * v.z)), fma(u.x, v.y, -(u.y * v.x))};
 }
+// Geometry-side reciprocal and reciprocal square root: the hardware v_rcp_f64 / v_rsq_f64
+// estimate plus two Newton-Raphson steps (quadratic convergence: full f64 accuracy, within an
+// ulp of the IEEE quotient, at about half the instructions of the IEEE division / sqrt
+// sequences). Used only where the operand is finite and non-zero by construction (quad
+// denominators past the 1e-8 test, |d|^2, |v|^2 of non-degenerate vectors); radiance weights
+// keep IEEE division so 0/0 stays NaN exactly as in the reference.
+__device__ __forceinline__ double rcp_nr(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  return fma(fma(-b, r, 1.0), r, r);
+}
+__device__ __forceinline__ double div_nr(double a, double b) {
+  double r = rcp_nr(b);
+  double q = a * r;
+  return fma(fma(-b, q, a), r, q);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double h = 0.5 * x;
+  y = y * fma(-h * y, y, 1.5);
+  return y * fma(-h * y, y, 1.5);
+}
 __device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
-  double inv = 1.0 / sqrt(dot(v, v));
-  return v * inv;
+  return v * rsq_nr(dot(v, v));
 }
 __device__ __forceinline__ d3 reflect(d3 v, d3 n) {  // vec3.rs:219-221
   return vfma(-2.0 * dot(v, n), n, v);
@@ -121,7 +151,7 @@ struct TraceParams {
   const uint32_t* __restrict__ lights;
   const uint32_t* __restrict__ light_offs;
   const uint8_t* __restrict__ texels;
-  float* __restrict__ partial;
+  float* __restrict__ samp;  // per-sample radiance [sj_local][row][x][s_i] x RGB
   unsigned long long* __restrict__ ops;
   uint32_t root, n_lights, lights_is_list, flags;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
@@ -167,6 +197,7 @@ __device__ __forceinline__ d3 arr3(const double* a) { return mk(a[0], a[1], a[2]
 template <bool COUNT>
 struct Ctr {
   __device__ __forceinline__ void inc(int) {}
+  __device__ __forceinline__ void inc_if(int, bool) {}
   __device__ __forceinline__ void flush(unsigned int*) {}
 };
 template <>
@@ -177,6 +208,7 @@ struct Ctr<true> {
     for (int k = 0; k < RT_OP_COUNT; ++k) c[k] = 0;
   }
   __device__ __forceinline__ void inc(int k) { c[k]++; }
+  __device__ __forceinline__ void inc_if(int k, bool b) { c[k] += b ? 1u : 0u; }
   __device__ void flush(unsigned int* sh) {
 #pragma unroll
     for (int k = 0; k < RT_OP_COUNT; ++k)
@@ -186,26 +218,28 @@ struct Ctr<true> {
 
 // ---------------------------------------------------------------- primitives
 // Quad::hit object.rs:453-490; inclusive interval (Interval::contains interval.rs:21-23).
+// Branch-free: every lane evaluates the whole test and the outcome is a predicate, so a wave
+// walks the quad in one straight-line block (no exec-mask churn, loads of the next node can be
+// hoisted). Rejections follow the reference's order and NaN behaviour exactly:
+// |n.d| < 1e-8 -> miss; !(tmin <= t <= tmax) -> miss; a < 0 || 1 < a || b < 0 || 1 < b -> miss.
 template <bool COUNT, class Ptr>
 __device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double tmax,
                                           double& t_out, Ctr<COUNT>& C) {
   C.inc(RT_OP_QUAD_TESTS);
   d3 n = ld3(q, 0);
   double denom = dot(n, d);
-  if (fabs(denom) < 1e-8) return false;
-  C.inc(RT_OP_QUAD_PLANE);
-  double t = (ldd(q, 3) - dot(n, o)) / denom;
-  if (!(tmin <= t && t <= tmax)) return false;
-  C.inc(RT_OP_QUAD_INTERVAL);
-  d3 p = vfma(t, d, o);
-  d3 pq = p - ld3(q, 4);
-  d3 w = ld3(q, 8);
-  double a = dot(w, cross(pq, ld3(q, 16)));
-  double b = dot(w, cross(ld3(q, 12), pq));
-  if (a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b) return false;
-  C.inc(RT_OP_QUAD_HITS);
-  t_out = t;
-  return true;
+  double t = div_nr(ldd(q, 3) - dot(n, o), denom);
+  d3 pq = vfma(t, d, o) - ld3(q, 4);
+  double a = dot(pq, ld3(q, 8));
+  double b = dot(pq, ld3(q, 12));
+  bool plane = !(fabs(denom) < 1e-8);
+  bool range = plane && (tmin <= t && t <= tmax);
+  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
+  C.inc_if(RT_OP_QUAD_PLANE, plane);
+  C.inc_if(RT_OP_QUAD_INTERVAL, range);
+  C.inc_if(RT_OP_QUAD_HITS, hit);
+  if (hit) t_out = t;
+  return hit;
 }
 
 // Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
@@ -224,9 +258,10 @@ __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double
   if (disc < 0.0) return false;
   C.inc(RT_OP_SPHERE_ROOTS);
   double sqrtd = sqrt(disc);
-  double root = (-half_b - sqrtd) / a;
+  double ra = rcp_nr(a);
+  double root = (-half_b - sqrtd) * ra;
   if (!(tmin < root && root < tmax)) {
-    root = (sqrtd - half_b) / a;
+    root = (sqrtd - half_b) * ra;
     if (!(tmin < root && root < tmax)) return false;
   }
   C.inc(RT_OP_SPHERE_HITS);
@@ -498,16 +533,6 @@ __device__ __noinline__ void sphere_uv(d3 p, double& u, double& v) {
 struct Onb {
   d3 u, v, w;
 };
-__device__ __forceinline__ Onb onb_from_w(d3 w) {  // onb.rs:32-47
-  Onb b;
-  d3 uw = unit_vector(w);
-  d3 a = fabs(uw.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
-  d3 v = unit_vector(cross(uw, a));
-  b.u = cross(uw, v);
-  b.v = v;
-  b.w = uw;
-  return b;
-}
 __device__ __forceinline__ d3 onb_local(const Onb& b, d3 a) {  // onb.rs:24-26
   return vfma(a.x, b.u, vfma(a.y, b.v, b.w * a.z));
 }
@@ -564,99 +589,92 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>&
   return P.lights_is_list ? sum * (1.0 / (double)P.n_lights) : sum;
 }
 
-// Light-list generate (HittablePDF::generate pdf.rs:95-97 -> HittableList::random
-// hittable.rs:126-129 -> Quad::random object.rs:503-506 / Sphere::random 204-212).
-__device__ d3 light_random(const TraceParams& P, d3 origin, Rng& g) {
-  uint32_t i = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
-  const uint32_t* L = P.lights + P.light_offs[i];
-  uint32_t type = L[0] & 0xffu;
-  if (type == RTL_QUAD) {
-    double a = rnd(g);
-    double b = rnd(g);
-    d3 p = vfma(b, ld3(L, 16), vfma(a, ld3(L, 12), ld3(L, 4)));
-    return p - origin;
-  }
-  if (type == RTL_SPHERE) {
-    d3 c = ld3(L, 0);
-    double r = ldd(L, 3);
-    d3 direction = c - origin;
-    double dist2 = dot(direction, direction);
-    Onb b = onb_from_w(direction);
-    double r1 = rnd(g), r2 = rnd(g);  // random_to_sphere object.rs:122-132
-    double z = fma(r2, sqrt(1.0 - r * r / dist2) - 1.0, 1.0);
-    double s, cc;
-    sincos2pi(r1, &s, &cc);
-    double sq = sqrt(fma(-z, z, 1.0));
-    return onb_local(b, mk(cc * sq, s * sq, z));
-  }
-  return mk(1., 0., 0.);
+__device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t slot, d3 L) {
+  float* o = samp + slot * 3;
+  o[0] = (float)L.x;
+  o[1] = (float)L.y;
+  o[2] = (float)L.z;
 }
 
 // ---------------------------------------------------------------- the path kernel
 // VOL: scene has ConstantMedium nodes; TEX: some material reads a non-solid texture.
 template <bool COUNT, bool VOL, bool TEX, bool UNI>
-__global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
+__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) {
   __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
   if (COUNT) {
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
     __syncthreads();
   }
   Ctr<COUNT> C;
-  const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   const int sjl = wave % P.n_sj;
   const int tile = wave / P.n_sj;
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const int x = tx * kWaveTile + (lane & 7);
-  const int kr = ty * kWaveTile + (lane >> 3);
-  const bool active = x < P.W && kr < P.n_rows;
-  const int y = P.row_begin + kr * P.row_step;
-  const uint32_t pixel = (uint32_t)(y * P.W + x);
+  const int tile_w = min(kWaveTile, P.W - tx * kWaveTile);
+  const int tile_h = min(kWaveTile, P.n_rows - ty * kWaveTile);
+  const int nv = tile_w * tile_h;          // valid pixels of the tile (wave-uniform)
+  const int pool = nv * P.sqrt_spp;        // paths of this wave
   const int s_j = P.sj0 + sjl;
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
 
-  d3 row = mk(0., 0., 0.);
   d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
   double tm = 0.;
   int depth = 0;
-  int s_i = 0;
   bool alive = false;
+  size_t slot = 0;  // per-sample output slot of the path in flight
+  int next = 0;     // pool items claimed so far (wave-uniform)
   Rng g = {0u, 0u, 0u, 0u};
 
   for (;;) {
-    if (!alive) {
-      if (!active || s_i >= P.sqrt_spp) break;
-      // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
-      g = rng_seed(P.seed_lo, P.seed_hi, pixel, (uint32_t)(s_j * P.sqrt_spp + s_i));
-      C.inc(RT_OP_SAMPLES);
-      d3 pc = vfma((double)y, arr3(P.dv), vfma((double)x, arr3(P.du), arr3(P.p00)));
-      double px = fma(P.rs, (double)s_i + rnd(g), -0.5);
-      double py = fma(P.rs, (double)s_j + rnd(g), -0.5);
-      d3 ps = pc + vfma(px, arr3(P.du), arr3(P.dv) * py);
-      d3 origin = arr3(P.center);
-      if (P.defocus) {
-        for (;;) {
-          double dx = rnd_pm1(g);
-          double dy = rnd_pm1(g);
-          if (fma(dx, dx, dy * dy) < 1.0) {
-            origin = vfma(dy, arr3(P.ddv), vfma(dx, arr3(P.ddu), arr3(P.center)));
-            break;
+    // ---- pool scheduling: every idle lane claims the next unclaimed item (all 64 lanes are
+    // active here: lanes only ever leave the loop together)
+    const bool idle = !alive;
+    const unsigned long long want = __ballot(idle);
+    if (idle) {
+      const int rank = (int)__builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+      const int k = next + rank;
+      if (k < pool) {
+        const int pv = k % nv, s_i = k / nv;
+        const int x = tx * kWaveTile + pv % tile_w;
+        const int kr = ty * kWaveTile + pv / tile_w;
+        const int y = P.row_begin + kr * P.row_step;
+        slot = (((size_t)sjl * P.n_rows + kr) * P.W + x) * (size_t)P.sqrt_spp + s_i;
+        // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
+        g = rng_seed(P.seed_lo, P.seed_hi, (uint32_t)(y * P.W + x),
+                     (uint32_t)(s_j * P.sqrt_spp + s_i));
+        C.inc(RT_OP_SAMPLES);
+        d3 pc = vfma((double)y, arr3(P.dv), vfma((double)x, arr3(P.du), arr3(P.p00)));
+        double px = fma(P.rs, (double)s_i + rnd(g), -0.5);
+        double py = fma(P.rs, (double)s_j + rnd(g), -0.5);
+        d3 ps = pc + vfma(px, arr3(P.du), arr3(P.dv) * py);
+        d3 origin = arr3(P.center);
+        if (P.defocus) {
+          for (;;) {
+            double dx = rnd_pm1(g);
+            double dy = rnd_pm1(g);
+            if (fma(dx, dx, dy * dy) < 1.0) {
+              origin = vfma(dy, arr3(P.ddv), vfma(dx, arr3(P.ddu), arr3(P.center)));
+              break;
+            }
           }
         }
+        ro = origin;
+        rd = ps - origin;
+        tm = rnd(g);
+        beta = mk(1., 1., 1.);
+        Lp = mk(0., 0., 0.);
+        depth = P.max_depth;
+        alive = true;
       }
-      ro = origin;
-      rd = ps - origin;
-      tm = rnd(g);
-      beta = mk(1., 1., 1.);
-      Lp = mk(0., 0., 0.);
-      depth = P.max_depth;
-      alive = true;
-      ++s_i;
     }
+    next += __popcll(want);
+    if (__ballot(alive) == 0ull) break;
+    if (!alive) continue;
     if (depth <= 0) {  // ray_color depth guard render.rs:260-262
       C.inc(RT_OP_DEPTH_CUTOFF);
-      row = row + Lp;
+      store_sample(P.samp, slot, Lp);
       alive = false;
       continue;
     }
@@ -668,7 +686,7 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
                                     hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * arr3(P.bg);
-      row = row + Lp;
+      store_sample(P.samp, slot, Lp);
       alive = false;
       continue;
     }
@@ -690,9 +708,8 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
       normal = front ? n : -n;
       if (needs_uv) {
         d3 pq = p - ld3(X, 4);
-        d3 w = ld3(X, 8);
-        u = dot(w, cross(pq, ld3(X, 16)));
-        v = dot(w, cross(ld3(X, 12), pq));
+        u = dot(pq, ld3(X, 8));
+        v = dot(pq, ld3(X, 12));
       }
     } else if (type == RTL_SPHERE) {
       d3 c = ld3(X, 0);
@@ -716,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, mh.y, u, v, p, C), Lp);
-      row = row + Lp;
+      store_sample(P.samp, slot, Lp);
       alive = false;
       continue;
     }
@@ -756,17 +773,58 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
     const bool iso = kind == RT_MAT_ISOTROPIC;
     C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
     d3 atten = tex_value<COUNT, TEX>(P, mh.y, u, v, p, C);
-    Onb uvw;
-    if (!iso) uvw = onb_from_w(normal);  // CosinePDF::new pdf.rs:58-62
-    d3 dir;
+    // Draw order as the reference: mixture coin (pdf.rs:120-126), then light index
+    // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
     bool light_branch = false;
-    if (have_lights) light_branch = rnd(g) < 0.5;  // MixturePDF::generate pdf.rs:120-126
+    if (have_lights) light_branch = rnd(g) < 0.5;
+    uint32_t ltype = 0;
+    gptr L = P.lights;
     if (light_branch) {
       C.inc(RT_OP_LIGHT_GEN);
-      dir = light_random(P, p, g);
+      uint32_t li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
+      L = P.lights + P.light_offs[li];
+      ltype = L[0] & 0xffu;
     } else {
       C.inc(RT_OP_COSINE_GEN);
-      dir = iso ? random_unit_vector(g) : onb_local(uvw, random_cosine_direction(g));
+    }
+    d3 dir;
+    const d3 un = unit_vector(normal);  // CosinePDF's w (pdf.rs:58-62, onb.rs:33)
+    if (iso && !light_branch) {
+      dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
+    } else if (light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
+      dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
+    } else {
+      // Quad::random (object.rs:503-506), Sphere::random / random_to_sphere (204-212, 122-132)
+      // and CosinePDF::generate (pdf.rs:75-77, vec3.rs:240-250) share one straight-line block:
+      // one ONB, one sincos, selects instead of divergent branches.
+      const double r1 = rnd(g), r2 = rnd(g);
+      const bool lq = light_branch && ltype == RTL_QUAD;
+      const bool ls = light_branch && ltype == RTL_SPHERE;
+      d3 c = ls ? ld3(L, 0) : p;
+      double rad = ls ? ldd(L, 3) : 0.0;
+      d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
+      double dist2 = dot(wdir, wdir);
+      d3 w = ls ? unit_vector(wdir) : un;
+      d3 aa = fabs(w.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
+      Onb b;
+      b.v = unit_vector(cross(w, aa));
+      b.u = cross(w, b.v);
+      b.w = w;
+      double sn, cs;
+      sincos2pi(r1, &sn, &cs);
+      double z, rho;
+      if (ls) {
+        z = fma(r2, sqrt(1.0 - rad * rad / dist2) - 1.0, 1.0);
+        rho = sqrt(fma(-z, z, 1.0));
+      } else {
+        z = sqrt(1.0 - r2);
+        rho = sqrt(r2);
+      }
+      d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
+      if (lq) {
+        local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
+      }
+      dir = local;
     }
     double mat_pdf, s_pdf;
     if (iso) {
@@ -774,7 +832,7 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
       s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
     } else {
       d3 udir = unit_vector(dir);
-      double cv = dot(udir, uvw.w) / kPi;            // CosinePDF::value pdf.rs:69-73
+      double cv = dot(udir, un) / kPi;               // CosinePDF::value pdf.rs:69-73
       mat_pdf = cv > 0.0 ? cv : 0.0;
       double cs = dot(normal, udir);                 // Lambertian::scattering_pdf 100-108
       s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
@@ -786,12 +844,6 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
     rd = dir;
     --depth;
   }
-  if (active) {
-    float* out = P.partial + ((size_t)(sjl * P.n_rows + kr) * P.W + x) * 3;
-    out[0] = (float)row.x;
-    out[1] = (float)row.y;
-    out[2] = (float)row.z;
-  }
   if (COUNT) {
     C.flush(sh_ops);
     __syncthreads();
@@ -800,16 +852,44 @@ __global__ __launch_bounds__(kBlock) void rt_trace(TraceParams P) {
   }
 }
 
-// Sum the per-stratum-row partials in s_j order (render.rs:185-189 accumulation), then add
-// into (or overwrite) the caller's raw-sum framebuffer.
-__global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ partial,
+// Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
+// order of render.rs:185-189, in f64. Chunked calls carry the running sum in `tot`.
+// mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite accum.
+__global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
+                                                 double* __restrict__ tot,
                                                  float* __restrict__ accum, int n_px, int n_sj,
-                                                 int overwrite) {
+                                                 int S, int mode) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_px * 3) return;
-  double s = 0.0;
-  for (int k = 0; k < n_sj; ++k) s += (double)partial[(size_t)k * n_px * 3 + i];
-  accum[i] = overwrite ? (float)s : (float)((double)accum[i] + s);
+  if (i >= n_px) return;
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  if (!(mode & 1)) {
+    t0 = tot[3 * i];
+    t1 = tot[3 * i + 1];
+    t2 = tot[3 * i + 2];
+  }
+  for (int k = 0; k < n_sj; ++k) {
+    const float* r = samp + ((size_t)k * n_px + i) * (size_t)S * 3;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+    for (int si = 0; si < S; ++si) {
+      r0 += (double)r[3 * si];
+      r1 += (double)r[3 * si + 1];
+      r2 += (double)r[3 * si + 2];
+    }
+    t0 += r0;
+    t1 += r1;
+    t2 += r2;
+  }
+  if (mode & 2) {
+    float* a = accum + 3 * i;
+    if (mode & 4) {
+      a[0] = (float)t0, a[1] = (float)t1, a[2] = (float)t2;
+    } else {
+      a[0] = (float)((double)a[0] + t0), a[1] = (float)((double)a[1] + t1);
+      a[2] = (float)((double)a[2] + t2);
+    }
+  } else {
+    tot[3 * i] = t0, tot[3 * i + 1] = t1, tot[3 * i + 2] = t2;
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -837,8 +917,8 @@ struct rt_scene {
   const uint32_t *nodes = nullptr, *mats = nullptr, *texs = nullptr, *lights = nullptr,
                  *light_offs = nullptr;
   const uint8_t *perlin = nullptr, *texels = nullptr;
-  float* partial = nullptr;
-  size_t partial_bytes = 0;
+  uint8_t* work = nullptr;  // per-sample radiance slots + f64 running sums (grown on demand)
+  size_t work_bytes = 0;
   unsigned long long* ops = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;
@@ -927,7 +1007,7 @@ void rt_scene_destroy(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
   if (sc->dev) (void)hipFree(sc->dev);
-  if (sc->partial) (void)hipFree(sc->partial);
+  if (sc->work) (void)hipFree(sc->work);
   if (sc->ops) (void)hipFree(sc->ops);
   if (sc->ev0) (void)hipEventDestroy(sc->ev0);
   if (sc->ev1) (void)hipEventDestroy(sc->ev1);
@@ -962,14 +1042,24 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   if (stats) std::memset(stats, 0, sizeof(*stats));
   const size_t n_px = (size_t)opts->n_rows * W;
   if (n_px == 0) return RT_OK;
-  const size_t need = n_px * 3 * sizeof(float) * (size_t)n_sj;
-  if (need > sc->partial_bytes) {
-    if (sc->partial) HIP_TRY(hipFree(sc->partial));
-    sc->partial = nullptr;
-    sc->partial_bytes = 0;
-    HIP_TRY(hipMalloc(&sc->partial, need));
-    sc->partial_bytes = need;
+  // Workspace: one float3 slot per sample of a chunk of stratum rows, plus an f64 running sum
+  // per pixel. Chunks keep it under RT_WORKSPACE_MB (default 8 GiB) even for the 3840x2160 x
+  // 10000 spp config; the C2 frame (800x800x961) fits one chunk (7.4 GB).
+  size_t cap = (size_t)8192 << 20;
+  if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
+  const size_t per_sj = n_px * (size_t)S * 3 * sizeof(float);
+  const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
+  int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_sj, (cap > tot_bytes ? cap - tot_bytes : 0) / per_sj));
+  const size_t need = tot_bytes + per_sj * (size_t)chunk;
+  if (need > sc->work_bytes) {
+    if (sc->work) HIP_TRY(hipFree(sc->work));
+    sc->work = nullptr;
+    sc->work_bytes = 0;
+    HIP_TRY(hipMalloc(&sc->work, need));
+    sc->work_bytes = need;
   }
+  double* tot = (double*)sc->work;
+  float* samp = (float*)(sc->work + tot_bytes);
   TraceParams P;
   std::memset(&P, 0, sizeof(P));
   P.nodes = sc->nodes;
@@ -979,7 +1069,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.lights = sc->lights;
   P.light_offs = sc->light_offs;
   P.texels = sc->texels;
-  P.partial = sc->partial;
+  P.samp = samp;
   P.ops = sc->ops;
   P.root = sc->hdr.root;
   P.n_lights = sc->hdr.n_lights;
@@ -1008,9 +1098,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.seed_hi = (uint32_t)(opts->seed >> 32);
   P.tiles_x = (W + kWaveTile - 1) / kWaveTile;
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
-  const int64_t waves = (int64_t)P.tiles_x * tiles_y * n_sj;
-  const int64_t blocks = (waves + (kBlock / 64) - 1) / (kBlock / 64);
-  if (blocks > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+  const int64_t waves_per_sj = (int64_t)P.tiles_x * tiles_y;
+  if ((waves_per_sj * chunk + 3) / 4 > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
   const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
@@ -1028,13 +1117,20 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
       rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
   kern_t kern = table[(count ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) + (uni ? 1 : 0)];
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
-  HIP_TRY(hipGetLastError());
+  for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
+    const int cn = std::min(chunk, sj0 + n_sj - c0);
+    P.sj0 = c0;
+    P.n_sj = cn;
+    const int64_t blocks = (waves_per_sj * cn + (kBlock / 64) - 1) / (kBlock / 64);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
+    HIP_TRY(hipGetLastError());
+    const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
+                     ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
+    hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, stream, samp,
+                       tot, accum, (int)n_px, cn, S, mode);
+    HIP_TRY(hipGetLastError());
+  }
   if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));
-  const int n3 = (int)(n_px * 3);
-  hipLaunchKernelGGL(rt_reduce, dim3((n3 + 255) / 256), dim3(256), 0, stream, sc->partial, accum,
-                     (int)n_px, n_sj, (opts->flags & RT_FLAG_OVERWRITE) ? 1 : 0);
-  HIP_TRY(hipGetLastError());
   if (stats) {
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.f;

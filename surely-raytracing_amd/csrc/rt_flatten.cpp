@@ -156,14 +156,23 @@ struct Emitter {
   }
   void quad(const Node& n, bool light) {
     if (!check_mat(n.mat) && !light) return;
-    size_t p = push(RTL_QUAD, RTL_QUAD_WORDS);
+    size_t p = push(RTL_QUAD, light ? RTL_LQUAD_WORDS : RTL_QUAD_WORDS);
     const double* f = n.f;  // q 0-2, u 3-5, v 6-8, n 9-11, w 12-14, d 15, area 16
+    const double u[3] = {f[3], f[4], f[5]}, v[3] = {f[6], f[7], f[8]}, wv[3] = {f[12], f[13], f[14]};
+    // A = v x w, B = w x u (triple-product form of the planar coordinates, rt_layout.h)
+    const double A[3] = {v[1] * wv[2] - v[2] * wv[1], v[2] * wv[0] - v[0] * wv[2],
+                         v[0] * wv[1] - v[1] * wv[0]};
+    const double B[3] = {wv[1] * u[2] - wv[2] * u[1], wv[2] * u[0] - wv[0] * u[2],
+                         wv[0] * u[1] - wv[1] * u[0]};
     w[p + 2] = (uint32_t)(n.mat < 0 ? 0 : n.mat);
     putd(w, p, 0, f[9]), putd(w, p, 1, f[10]), putd(w, p, 2, f[11]), putd(w, p, 3, f[15]);
     putd(w, p, 4, f[0]), putd(w, p, 5, f[1]), putd(w, p, 6, f[2]), putd(w, p, 7, f[16]);
-    putd(w, p, 8, f[12]), putd(w, p, 9, f[13]), putd(w, p, 10, f[14]);
-    putd(w, p, 12, f[3]), putd(w, p, 13, f[4]), putd(w, p, 14, f[5]);
-    putd(w, p, 16, f[6]), putd(w, p, 17, f[7]), putd(w, p, 18, f[8]);
+    putd(w, p, 8, A[0]), putd(w, p, 9, A[1]), putd(w, p, 10, A[2]);
+    putd(w, p, 12, B[0]), putd(w, p, 13, B[1]), putd(w, p, 14, B[2]);
+    if (light) {
+      putd(w, p, 16, u[0]), putd(w, p, 17, u[1]), putd(w, p, 18, u[2]);
+      putd(w, p, 20, v[0]), putd(w, p, 21, v[1]), putd(w, p, 22, v[2]);
+    }
   }
   void sphere(const Node& n, bool light) {
     if (!check_mat(n.mat) && !light) return;

@@ -30,10 +30,15 @@
 /* header word 0: type | (flags << 8); word 1: skip (next node after the subtree).
  * Payloads are f64 (the reference computes in f64) starting at word 4, read as
  * 16-byte double2 pairs. dN = double index N counted from word 4. */
-/* QUAD (44 words): [hdr][skip][mat][0] d0-1 n.xy | d2-3 n.z,D | d4-5 q.xy | d6-7 q.z,area |
- *   d8-9 w.xy | d10-11 w.z,0 | d12-13 u.xy | d14-15 u.z,0 | d16-17 v.xy | d18-19 v.z,0
- *                                                                        object.rs:414-446 */
-#define RTL_QUAD_WORDS 44
+/* QUAD (36 words): [hdr][skip][mat][0] d0-1 n.xy | d2-3 n.z,D | d4-5 q.xy | d6-7 q.z,area |
+ *   d8-9 A.xy | d10-11 A.z,0 | d12-13 B.xy | d14-15 B.z,0      with A = v x w, B = w x u, so
+ *   the planar coordinates of object.rs:469-470, a = w.(pq x v) and b = w.(u x pq), are the
+ *   same triple products evaluated as a = pq.A, b = pq.B (two dots instead of two crosses and
+ *   two dots per test).                                                  object.rs:414-490
+ * Light records (LQUAD, 52 words) append d16-19 u.xyz,0 and d20-23 v.xyz,0 for Quad::random
+ * (object.rs:503-506). */
+#define RTL_QUAD_WORDS 36
+#define RTL_LQUAD_WORDS 52
 /* SPHERE (20 words): [hdr][skip][mat][moving] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r  object.rs:73-105 */
 #define RTL_SPHERE_WORDS 20
 /* BVH (16 words): [hdr][skip][0][0] d0-5 xmin xmax ymin ymax zmin zmax     hittable.rs:135-187 */

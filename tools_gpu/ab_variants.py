@@ -1,0 +1,40 @@
+"""A/B the library variants under build/variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24). Usage: python tools_gpu/ab_variants.py [width spp rounds]"""
+import ctypes as C
+import glob
+import sys
+import time
+
+sys.path.insert(0, "surely-raytracing_amd")
+import numpy as np  # noqa: E402
+import surely_rt as rt  # noqa: E402
+
+W = int(sys.argv[1]) if len(sys.argv) > 1 else 800
+SPP = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+ROUNDS = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+SCENE = sys.argv[4] if len(sys.argv) > 4 else "cornell_box"
+paths = sorted(glob.glob("build/variants/*.so")) + ["build/librtmi355x.so"]
+blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
+libs, scenes = [], []
+for p in paths:
+    lib = rt.load_device_lib(p)
+    h = C.c_void_p()
+    assert lib.rt_scene_create(blob.ref(), 0, C.byref(h)) == 0, lib.rt_last_error()
+    libs.append(lib)
+    scenes.append(h)
+opts = rt.make_opts(cam, seed=1)
+res = {p: [] for p in paths}
+ref = None
+for r in range(ROUNDS + 1):
+    for p, lib, h in zip(paths, libs, scenes):
+        acc = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
+        st = rt.RtStats()
+        assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
+        if ref is None:
+            ref = acc
+        same = np.array_equal(acc, ref)
+        if r > 0:
+            res[p].append(st.ms_kernel)
+        if r == ROUNDS:
+            print(f"{p:45s} kernel ms min {min(res[p]):9.2f} med {np.median(res[p]):9.2f}  "
+                  f"Msamples/s {st.samples / min(res[p]) / 1e3:8.1f}  same_as_first {same}", flush=True)
