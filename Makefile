@@ -51,6 +51,6 @@ clean:
 VARIANTS := $(BUILD)/variants
 variants: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(VARIANTS)
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=1 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w1.so
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=3 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w3.so
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=4 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_w4.so
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TRAV2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_trav2.so
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so
+	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so

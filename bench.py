@@ -176,7 +176,7 @@ def main():
         if ops is not None:
             # flops / bytes of the rank-0 launch (its share of rows) over its kernel time
             fl = roofline.flops(ops)
-            by = roofline.scene_bytes(ops, partial_bytes=n * W * 12 * cam.sqrt_spp)
+            by = roofline.scene_bytes(ops, partial_bytes=n * W * spp * 24)  # sample slots w+r
             ach = fl / (kernel_ms * 1e-3) / 1e12
             traffic = None
             tf = REPO / "profiles" / "pmc_traffic.json"

@@ -151,7 +151,7 @@ struct TraceParams {
   const uint32_t* __restrict__ lights;
   const uint32_t* __restrict__ light_offs;
   const uint8_t* __restrict__ texels;
-  float* __restrict__ samp;  // per-sample radiance [sj_local][row][x][s_i] x RGB
+  float* __restrict__ samp;  // per-sample radiance, [wave][pool item] x RGB (item = s_i*nv + pv)
   unsigned long long* __restrict__ ops;
   uint32_t root, n_lights, lights_is_list, flags;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
@@ -360,6 +360,22 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
         }
       }
       node += RTL_QUAD_WORDS;
+    } else if (type == RTL_QUADS) {
+      // batch of sibling quads: the same sequential closest-hit updates as the list
+      const uint32_t cnt = h.x >> 8;
+      Ptr Q = X + 4;
+      for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
+        double t;
+        if (quad_test<COUNT>(Q, o, d, tmin, closest, t, C)) {
+          closest = t;
+          hit = true;
+          if (MAIN) {
+            hit_node = (uint32_t)(node + 4 + k * RTL_QUAD_WORDS);
+            hit_frame = frame;
+          }
+        }
+      }
+      node = h.y;
     } else if (type == RTL_SPHERE) {
       double t;
       if (sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C)) {
@@ -640,7 +656,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
         const int x = tx * kWaveTile + pv % tile_w;
         const int kr = ty * kWaveTile + pv / tile_w;
         const int y = P.row_begin + kr * P.row_step;
-        slot = (((size_t)sjl * P.n_rows + kr) * P.W + x) * (size_t)P.sqrt_spp + s_i;
+        slot = (size_t)wave * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
         // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
         g = rng_seed(P.seed_lo, P.seed_hi, (uint32_t)(y * P.W + x),
                      (uint32_t)(s_j * P.sqrt_spp + s_i));
@@ -682,6 +698,19 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     double t;
     uint32_t hn = 0;
     int hf = -1;
+#ifdef RT_ABL_TRAV2  // ablation build: the traversal runs twice (same result); the time delta
+                     // is the traversal's cost
+    {
+      double z = 0.0;
+      asm volatile("" : "+v"(z));
+      double t2;
+      uint32_t hn2;
+      int hf2;
+      traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001 + z, INFINITY, t2,
+                                      hn2, hf2, g, C);
+      asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
+    }
+#endif
     if (!traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
                                     hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
@@ -838,7 +867,9 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
     }
     double pdf_val = mat_pdf;
+#ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
     if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, C), 0.5 * mat_pdf);  // pdf.rs:116
+#endif
     beta = beta * (atten * (s_pdf / pdf_val));
     ro = p;
     rd = dir;
@@ -853,34 +884,43 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
-// order of render.rs:185-189, in f64. Chunked calls carry the running sum in `tot`.
-// mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite accum.
+// order of render.rs:185-189, in f64. Samples sit in pool-item order per wave (item =
+// s_i * nv + pv), so neighbouring pixels read neighbouring slots. Chunked calls carry the
+// running sum in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite.
 __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
                                                  double* __restrict__ tot,
-                                                 float* __restrict__ accum, int n_px, int n_sj,
-                                                 int S, int mode) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_px) return;
+                                                 float* __restrict__ accum, int W, int n_rows,
+                                                 int tiles_x, int n_sj, int S, int mode) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * n_rows) return;
+  const int x = i % W, kr = i / W;
+  const int tx = x / kWaveTile, ty = kr / kWaveTile;
+  const int tile_w = min(kWaveTile, W - tx * kWaveTile);
+  const int tile_h = min(kWaveTile, n_rows - ty * kWaveTile);
+  const int nv = tile_w * tile_h;
+  const int pv = (kr - ty * kWaveTile) * tile_w + (x - tx * kWaveTile);
+  const size_t tile = (size_t)ty * tiles_x + tx;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   if (!(mode & 1)) {
-    t0 = tot[3 * i];
-    t1 = tot[3 * i + 1];
-    t2 = tot[3 * i + 2];
+    t0 = tot[3 * (size_t)i];
+    t1 = tot[3 * (size_t)i + 1];
+    t2 = tot[3 * (size_t)i + 2];
   }
   for (int k = 0; k < n_sj; ++k) {
-    const float* r = samp + ((size_t)k * n_px + i) * (size_t)S * 3;
+    const float* r = samp + ((tile * n_sj + k) * (size_t)(kWaveTile * kWaveTile) * S + pv) * 3;
     double r0 = 0.0, r1 = 0.0, r2 = 0.0;
     for (int si = 0; si < S; ++si) {
-      r0 += (double)r[3 * si];
-      r1 += (double)r[3 * si + 1];
-      r2 += (double)r[3 * si + 2];
+      const float* q = r + (size_t)si * nv * 3;
+      r0 += (double)q[0];
+      r1 += (double)q[1];
+      r2 += (double)q[2];
     }
     t0 += r0;
     t1 += r1;
     t2 += r2;
   }
+  float* a = accum + 3 * (size_t)i;
   if (mode & 2) {
-    float* a = accum + 3 * i;
     if (mode & 4) {
       a[0] = (float)t0, a[1] = (float)t1, a[2] = (float)t2;
     } else {
@@ -888,7 +928,7 @@ __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
       a[2] = (float)((double)a[2] + t2);
     }
   } else {
-    tot[3 * i] = t0, tot[3 * i + 1] = t1, tot[3 * i + 2] = t2;
+    tot[3 * (size_t)i] = t0, tot[3 * (size_t)i + 1] = t1, tot[3 * (size_t)i + 2] = t2;
   }
 }
 
@@ -1047,7 +1087,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   // 10000 spp config; the C2 frame (800x800x961) fits one chunk (7.4 GB).
   size_t cap = (size_t)8192 << 20;
   if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
-  const size_t per_sj = n_px * (size_t)S * 3 * sizeof(float);
+  const size_t n_tiles = (size_t)((W + kWaveTile - 1) / kWaveTile) *
+                         (size_t)((opts->n_rows + kWaveTile - 1) / kWaveTile);
+  const size_t per_sj = n_tiles * (size_t)(kWaveTile * kWaveTile) * (size_t)S * 3 * sizeof(float);
   const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
   int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_sj, (cap > tot_bytes ? cap - tot_bytes : 0) / per_sj));
   const size_t need = tot_bytes + per_sj * (size_t)chunk;
@@ -1127,7 +1169,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
                      ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
     hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, stream, samp,
-                       tot, accum, (int)n_px, cn, S, mode);
+                       tot, accum, W, opts->n_rows, P.tiles_x, cn, S, mode);
     HIP_TRY(hipGetLastError());
   }
   if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));

@@ -198,9 +198,28 @@ struct Emitter {
   void emit(const Node& n, int frame, std::vector<uint32_t>& chain, bool in_volume) {
     if (status != RT_OK) return;
     switch (n.tag) {
-      case RT_OBJ_LIST:
-        for (auto& k : n.kids) emit(*k, frame, chain, in_volume);
+      case RT_OBJ_LIST: {
+        // Runs of >= 2 sibling quads become one QUADS batch (same visiting order; no skip
+        // link can land inside a run because siblings of a list are never BVH boundaries).
+        size_t i = 0;
+        while (i < n.kids.size()) {
+          size_t j = i;
+          while (j < n.kids.size() && n.kids[j]->tag == RT_OBJ_QUAD) ++j;
+#ifdef RT_NO_QUADS
+          j = i;
+#endif
+          if (j - i >= 2) {
+            size_t p = push(RTL_QUADS | (uint32_t)((j - i) << 8), 4);
+            for (size_t k = i; k < j; ++k) quad(*n.kids[k], false);
+            w[p + 1] = (uint32_t)w.size();
+            i = j;
+          } else {
+            emit(*n.kids[i], frame, chain, in_volume);
+            ++i;
+          }
+        }
         break;
+      }
       case RT_OBJ_BVH: {
         has_bvh = true;
         size_t p = push(RTL_BVH, RTL_BVH_WORDS);

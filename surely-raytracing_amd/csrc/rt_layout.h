@@ -27,6 +27,8 @@
 #define RTL_EXIT 6
 #define RTL_VOLUME 7
 #define RTL_OTHER 8 /* light entry whose pdf_value is 0 (Object default arm, object.rs:295-311) */
+#define RTL_QUADS 9 /* batch of consecutive sibling quads: header word 0 = type | count << 8, then
+                       `count` QUAD records; traversed in order, exactly like the list it replaces */
 /* header word 0: type | (flags << 8); word 1: skip (next node after the subtree).
  * Payloads are f64 (the reference computes in f64) starting at word 4, read as
  * 16-byte double2 pairs. dN = double index N counted from word 4. */
