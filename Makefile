@@ -54,3 +54,8 @@ variants: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TRAV2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_trav2.so
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so
 	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so
+
+# section-cycle profiling build (tools_gpu/prof_sections.py); not shipped
+prof: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/prof
+	$(HIPCC) $(HIPFLAGS) -DRT_PROF -shared $(DEV_SRC) -o $(BUILD)/prof/librtmi355x.so

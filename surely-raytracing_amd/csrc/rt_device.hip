@@ -162,6 +162,19 @@ struct TraceParams {
   int tiles_x;
 };
 
+// The kernel's only argument sits at offset 0 of the kernarg segment. Camera constants are read
+// through this pointer at their point of use; the empty asm makes the pointer opaque so the loads
+// are not hoisted out of the path loop, where ~40 loop-invariant SGPRs would spill to VGPR lanes.
+typedef const __attribute__((address_space(4))) TraceParams* kparams_t;
+__device__ __forceinline__ kparams_t kparams() {
+  kparams_t p = (kparams_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ d3 karr3(const __attribute__((address_space(4))) double* a) {
+  return {a[0], a[1], a[2]};
+}
+
 // ---------------------------------------------------------------- loads
 // Two pointer kinds reach the same node records:
 //  gptr: per-lane (divergent) node index -> vector loads (global_load_dwordx4 through L1/L2)
@@ -622,6 +635,22 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     __syncthreads();
   }
   Ctr<COUNT> C;
+#ifdef RT_PROF  // profiling build: wave cycles per loop section into P.ops[0..7] (not shipped)
+  unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof_last = __builtin_readcyclecounter();
+  int prof_sec = 0;
+#define PROF(k)                                                  \
+  do {                                                           \
+    const unsigned long long now_ = __builtin_readcyclecounter(); \
+    prof_acc[prof_sec] += now_ - prof_last;                      \
+    prof_last = now_;                                            \
+    prof_sec = (k);                                              \
+  } while (0)
+#else
+#define PROF(k) \
+  do {          \
+  } while (0)
+#endif
   const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   const int sjl = wave % P.n_sj;
   const int tile = wave / P.n_sj;
@@ -643,6 +672,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
   Rng g = {0u, 0u, 0u, 0u};
 
   for (;;) {
+    PROF(0);
     // ---- pool scheduling: every idle lane claims the next unclaimed item (all 64 lanes are
     // active here: lanes only ever leave the loop together)
     const bool idle = !alive;
@@ -652,26 +682,39 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
           (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
       const int k = next + rank;
       if (k < pool) {
-        const int pv = k % nv, s_i = k / nv;
-        const int x = tx * kWaveTile + pv % tile_w;
-        const int kr = ty * kWaveTile + pv / tile_w;
-        const int y = P.row_begin + kr * P.row_step;
+        int pv, s_i, px_, py_;
+        if (nv == kWaveTile * kWaveTile) {  // full tile (wave-uniform): shifts
+          pv = k & (kWaveTile * kWaveTile - 1);
+          s_i = k >> 6;
+          px_ = pv & (kWaveTile - 1);
+          py_ = pv >> 3;
+        } else {
+          pv = k % nv;
+          s_i = k / nv;
+          px_ = pv % tile_w;
+          py_ = pv / tile_w;
+        }
+        const kparams_t Q = kparams();
+        const int x = tx * kWaveTile + px_;
+        const int kr = ty * kWaveTile + py_;
+        const int y = Q->row_begin + kr * Q->row_step;
         slot = (size_t)wave * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
         // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
-        g = rng_seed(P.seed_lo, P.seed_hi, (uint32_t)(y * P.W + x),
-                     (uint32_t)(s_j * P.sqrt_spp + s_i));
+        g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
+                     (uint32_t)(s_j * Q->sqrt_spp + s_i));
         C.inc(RT_OP_SAMPLES);
-        d3 pc = vfma((double)y, arr3(P.dv), vfma((double)x, arr3(P.du), arr3(P.p00)));
-        double px = fma(P.rs, (double)s_i + rnd(g), -0.5);
-        double py = fma(P.rs, (double)s_j + rnd(g), -0.5);
-        d3 ps = pc + vfma(px, arr3(P.du), arr3(P.dv) * py);
-        d3 origin = arr3(P.center);
-        if (P.defocus) {
+        d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
+        double px = fma(Q->rs, (double)s_i + rnd(g), -0.5);
+        double py = fma(Q->rs, (double)s_j + rnd(g), -0.5);
+        d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
+        d3 origin = karr3(Q->center);
+        if (Q->defocus) {
           for (;;) {
             double dx = rnd_pm1(g);
             double dy = rnd_pm1(g);
             if (fma(dx, dx, dy * dy) < 1.0) {
-              origin = vfma(dy, arr3(P.ddv), vfma(dx, arr3(P.ddu), arr3(P.center)));
+              const kparams_t R = kparams();
+              origin = vfma(dy, karr3(R->ddv), vfma(dx, karr3(R->ddu), karr3(R->center)));
               break;
             }
           }
@@ -695,6 +738,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       continue;
     }
     C.inc(RT_OP_WORLD_QUERIES);
+    PROF(1);
     double t;
     uint32_t hn = 0;
     int hf = -1;
@@ -714,12 +758,13 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     if (!traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
                                     hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
-      Lp = Lp + beta * arr3(P.bg);
+      Lp = Lp + beta * karr3(kparams()->bg);
       store_sample(P.samp, slot, Lp);
       alive = false;
       continue;
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
+    PROF(2);
     const uint32_t* X = P.nodes + hn;
     uint32_t type = X[0] & 0xffu;
     d3 o, d;
@@ -759,6 +804,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
         if ((uint32_t)k < fh.z) xform_out(P.nodes + c4[k], p, normal);
     }
     const uint32_t kind = mh.x & 0xffu;
+    PROF(3);
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, mh.y, u, v, p, C), Lp);
@@ -799,6 +845,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       continue;
     }
     // Lambertian / Isotropic: mixture-PDF branch render.rs:278-292
+    PROF(4);
     const bool iso = kind == RT_MAT_ISOTROPIC;
     C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
     d3 atten = tex_value<COUNT, TEX>(P, mh.y, u, v, p, C);
@@ -867,14 +914,22 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
     }
     double pdf_val = mat_pdf;
+    PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
     if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, C), 0.5 * mat_pdf);  // pdf.rs:116
 #endif
+    PROF(6);
     beta = beta * (atten * (s_pdf / pdf_val));
     ro = p;
     rd = dir;
     --depth;
   }
+#ifdef RT_PROF
+  PROF(7);
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&P.ops[k], prof_acc[k]);
+#endif
+#undef PROF
   if (COUNT) {
     C.flush(sh_ops);
     __syncthreads();
@@ -1142,7 +1197,11 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
   const int64_t waves_per_sj = (int64_t)P.tiles_x * tiles_y;
   if ((waves_per_sj * chunk + 3) / 4 > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+#ifdef RT_PROF
+  const bool count = true;
+#else
   const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
+#endif
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
   const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
@@ -1158,7 +1217,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       rt_trace<true, false, true, false>,   rt_trace<true, false, true, true>,
       rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
       rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
-  kern_t kern = table[(count ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) + (uni ? 1 : 0)];
+  kern_t kern = table[((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) + (uni ? 1 : 0)];
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
     const int cn = std::min(chunk, sj0 + n_sj - c0);
     P.sj0 = c0;

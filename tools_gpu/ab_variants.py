@@ -13,7 +13,7 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 else 800
 SPP = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 ROUNDS = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 SCENE = sys.argv[4] if len(sys.argv) > 4 else "cornell_box"
-paths = sorted(glob.glob("build/variants/*.so")) + ["build/librtmi355x.so"]
+paths = ["build/librtmi355x.so"] + sorted(glob.glob("build/variants/*.so"))
 blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
 libs, scenes = [], []
 for p in paths:
@@ -37,4 +37,4 @@ for r in range(ROUNDS + 1):
             res[p].append(st.ms_kernel)
         if r == ROUNDS:
             print(f"{p:45s} kernel ms min {min(res[p]):9.2f} med {np.median(res[p]):9.2f}  "
-                  f"Msamples/s {st.samples / min(res[p]) / 1e3:8.1f}  same_as_first {same}", flush=True)
+                  f"Msamples/s {st.samples / min(res[p]) / 1e3:8.1f}  same_as_default {same}", flush=True)

@@ -1,0 +1,27 @@
+"""Wave-cycle split of the path loop by section (build/prof, -DRT_PROF; not shipped).
+Usage: python tools_gpu/prof_sections.py [scene width spp]"""
+import ctypes as C
+import sys
+
+sys.path.insert(0, "surely-raytracing_amd")
+import numpy as np  # noqa: E402
+import surely_rt as rt  # noqa: E402
+
+NAMES = ["pool/regen", "traverse", "hit record", "emit/metal/dielectric", "lambert sample",
+         "light pdf", "beta update", "exit"]
+scene = sys.argv[1] if len(sys.argv) > 1 else "cornell_box"
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 800
+spp = int(sys.argv[3]) if len(sys.argv) > 3 else 100
+lib = rt.load_device_lib("build/prof/librtmi355x.so")
+blob, cam = rt.preset_blob(scene, width=W, spp=spp)
+h = C.c_void_p()
+assert lib.rt_scene_create(blob.ref(), 0, C.byref(h)) == 0, lib.rt_last_error()
+opts = rt.make_opts(cam, seed=1)
+for rep in range(2):
+    acc = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
+    st = rt.RtStats()
+    assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
+cyc = np.array([st.ops[k] for k in range(8)], dtype=np.float64)
+print(f"{scene} {W} spp {cam.samples_per_pixel}: kernel {st.ms_kernel:.2f} ms (profiling build)")
+for n, c in zip(NAMES, cyc):
+    print(f"  {n:24s} {100 * c / cyc.sum():6.2f} %   {c / st.samples:9.1f} wave-cyc/sample")
