@@ -153,6 +153,8 @@ struct TraceParams {
   const uint8_t* __restrict__ texels;
   float* __restrict__ samp;  // per-sample radiance, [wave][pool item] x RGB (item = s_i*nv + pv)
   unsigned long long* __restrict__ ops;
+  unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
+  int n_pools;                       // pools of this launch: tiles x n_sj
   uint32_t root, n_lights, lights_is_list, flags;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
@@ -253,6 +255,58 @@ __device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double
   C.inc_if(RT_OP_QUAD_HITS, hit);
   if (hit) t_out = t;
   return hit;
+}
+
+// The same test for an axis-aligned quad (rt_layout.h RTL_QUAD_AXIS): bit-identical results,
+// with r = rcp_nr(d) computed once per batch instead of once per quad.
+template <int K>
+__device__ __forceinline__ double comp(d3 v) {
+  return K == 0 ? v.x : (K == 1 ? v.y : v.z);
+}
+__device__ __forceinline__ double hilo(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
+}
+struct AQuad {  // the first 64 bytes of a world QUAD record
+  uint32_t h0;
+  double qk, qlo, clo, qhi, chi;
+};
+template <class Ptr>
+__device__ __forceinline__ AQuad load_aquad(Ptr Q) {
+  const uint4 a = ld4u(Q), b = ld4u(Q + 4), c = ld4u(Q + 8), e = ld4u(Q + 12);
+  return {a.x, hilo(b.x, b.y), hilo(b.z, b.w), hilo(c.x, c.y), hilo(c.z, c.w), hilo(e.x, e.y)};
+}
+template <bool COUNT, int K>
+__device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, double tmin,
+                                           double tmax, double& t_out, Ctr<COUNT>& C) {
+  constexpr int LO = K == 0 ? 1 : 0, HI = K == 2 ? 1 : 2;
+  C.inc(RT_OP_QUAD_TESTS);
+  const double dk = comp<K>(d), rk = comp<K>(r);
+  const double num = q.qk - comp<K>(o);
+  const double t0 = num * rk;
+  const double t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
+  const double a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
+  const double b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
+  bool plane = !(fabs(dk) < 1e-8);
+  bool range = plane && (tmin <= t && t <= tmax);
+  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
+  C.inc_if(RT_OP_QUAD_PLANE, plane);
+  C.inc_if(RT_OP_QUAD_INTERVAL, range);
+  C.inc_if(RT_OP_QUAD_HITS, hit);
+  if (hit) t_out = t;
+  return hit;
+}
+// A world QUAD record (batch member or single): branch on its axis code (wave-uniform in UNI
+// traversal); r = rcp_nr(d) of the current frame.
+template <bool COUNT, class Ptr>
+__device__ __forceinline__ bool world_quad_test(Ptr Q, d3 o, d3 d, d3 r, double tmin, double tmax,
+                                                double& t_out, Ctr<COUNT>& C) {
+  const AQuad q = load_aquad(Q);
+  switch (RTL_QUAD_AXIS(q.h0)) {
+    case 1u: return aquad_test<COUNT, 0>(q, o, d, r, tmin, tmax, t_out, C);
+    case 2u: return aquad_test<COUNT, 1>(q, o, d, r, tmin, tmax, t_out, C);
+    case 3u: return aquad_test<COUNT, 2>(q, o, d, r, tmin, tmax, t_out, C);
+    default: return quad_test<COUNT>(Q + RTL_QUAD_GEN, o, d, tmin, tmax, t_out, C);
+  }
 }
 
 // Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
@@ -364,7 +418,8 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
     uint32_t type = h.x & 0xffu;
     if (type == RTL_QUAD) {
       double t;
-      if (quad_test<COUNT>(X, o, d, tmin, closest, t, C)) {
+      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+      if (world_quad_test<COUNT>(X, o, d, r, tmin, closest, t, C)) {
         closest = t;
         hit = true;
         if (MAIN) {
@@ -377,9 +432,10 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
       // batch of sibling quads: the same sequential closest-hit updates as the list
       const uint32_t cnt = h.x >> 8;
       Ptr Q = X + 4;
+      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
         double t;
-        if (quad_test<COUNT>(Q, o, d, tmin, closest, t, C)) {
+        if (world_quad_test<COUNT>(Q, o, d, r, tmin, closest, t, C)) {
           closest = t;
           hit = true;
           if (MAIN) {
@@ -639,6 +695,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
   unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_last = __builtin_readcyclecounter();
   int prof_sec = 0;
+  unsigned long long prof_lanes = 0, prof_iters = 0;  // lanes entering traversal, wave-iterations
 #define PROF(k)                                                  \
   do {                                                           \
     const unsigned long long now_ = __builtin_readcyclecounter(); \
@@ -651,15 +708,12 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
   do {          \
   } while (0)
 #endif
-  const int wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  const int sjl = wave % P.n_sj;
-  const int tile = wave / P.n_sj;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const int tile_w = min(kWaveTile, P.W - tx * kWaveTile);
-  const int tile_h = min(kWaveTile, P.n_rows - ty * kWaveTile);
-  const int nv = tile_w * tile_h;          // valid pixels of the tile (wave-uniform)
-  const int pool = nv * P.sqrt_spp;        // paths of this wave
-  const int s_j = P.sj0 + sjl;
+  // Persistent waves: a wave takes pools (one 8x8 tile x one stratum row s_j: nv * sqrt_spp
+  // paths) from a global queue and its lanes claim paths across pool boundaries, so lanes only
+  // idle at the very end of the launch. Wave-uniform pool state:
+  const int lane = threadIdx.x & 63;
+  int pool_id = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_j = 0;
+  bool more = true;  // the queue may still hold pools
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
 
@@ -677,6 +731,25 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     // active here: lanes only ever leave the loop together)
     const bool idle = !alive;
     const unsigned long long want = __ballot(idle);
+    if (want != 0ull && next >= pool && more) {  // current pool drained: take the next one
+      uint32_t id = 0u;
+      if (lane == 0) id = atomicAdd(P.queue, 1u);
+      id = __builtin_amdgcn_readfirstlane(id);
+      if ((int)id < P.n_pools) {
+        pool_id = (int)id;
+        const int tile = pool_id / P.n_sj;
+        tx = tile % P.tiles_x;
+        ty = tile / P.tiles_x;
+        tile_w = min(kWaveTile, P.W - tx * kWaveTile);
+        nv = tile_w * min(kWaveTile, P.n_rows - ty * kWaveTile);
+        pool = nv * P.sqrt_spp;
+        s_j = P.sj0 + pool_id % P.n_sj;
+      } else {
+        more = false;
+        pool = 0;
+      }
+      next = 0;
+    }
     if (idle) {
       const int rank = (int)__builtin_amdgcn_mbcnt_hi(
           (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -698,7 +771,7 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
         const int x = tx * kWaveTile + px_;
         const int kr = ty * kWaveTile + py_;
         const int y = Q->row_begin + kr * Q->row_step;
-        slot = (size_t)wave * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
+        slot = (size_t)pool_id * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
         // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
         g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
                      (uint32_t)(s_j * Q->sqrt_spp + s_i));
@@ -729,7 +802,10 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       }
     }
     next += __popcll(want);
-    if (__ballot(alive) == 0ull) break;
+    if (__ballot(alive) == 0ull) {
+      if (!more) break;
+      continue;
+    }
     if (!alive) continue;
     if (depth <= 0) {  // ray_color depth guard render.rs:260-262
       C.inc(RT_OP_DEPTH_CUTOFF);
@@ -739,6 +815,10 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     }
     C.inc(RT_OP_WORLD_QUERIES);
     PROF(1);
+#ifdef RT_PROF
+    prof_lanes += __popcll(__ballot(1));
+    prof_iters += 1;
+#endif
     double t;
     uint32_t hn = 0;
     int hf = -1;
@@ -777,13 +857,14 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     uint4 mh = ld4u(M);
     const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
     if (type == RTL_QUAD) {
-      d3 n = ld3(X, 0);
+      const gptr XG = X + RTL_QUAD_GEN;
+      d3 n = ld3(XG, 0);
       front = dot(d, n) < 0.0;  // set_face_normal hittable.rs:22-37
       normal = front ? n : -n;
       if (needs_uv) {
-        d3 pq = p - ld3(X, 4);
-        u = dot(pq, ld3(X, 8));
-        v = dot(pq, ld3(X, 12));
+        d3 pq = p - ld3(XG, 4);
+        u = dot(pq, ld3(XG, 8));
+        v = dot(pq, ld3(XG, 12));
       }
     } else if (type == RTL_SPHERE) {
       d3 c = ld3(X, 0);
@@ -825,15 +906,13 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
     }
     if (kind == RT_MAT_DIELECTRIC) {  // material.rs:166-191
       C.inc(RT_OP_DIELECTRIC);
-      double ir = ldd(M, 3);
-      double ratio = front ? 1.0 / ir : ir;
+      double ratio = front ? ldd(M, 4) : ldd(M, 3);  // 1/ir : ir
       d3 ud = unit_vector(rd);
       double cos_t = fmin(dot(-ud, normal), 1.0);
       double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
       bool refl = ratio * sin_t > 1.0;
       if (!refl) {
-        double r0 = (1.0 - ratio) / (1.0 + ratio);
-        r0 = r0 * r0;
+        double r0 = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
         double xx = 1.0 - cos_t;
         double x2 = xx * xx;
         refl = fma(1.0 - r0, x2 * x2 * xx, r0) > rnd(g);
@@ -928,6 +1007,10 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
   PROF(7);
   if ((threadIdx.x & 63) == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(&P.ops[k], prof_acc[k]);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&P.ops[8], prof_lanes);
+    atomicAdd(&P.ops[9], prof_iters);
+  }
 #endif
 #undef PROF
   if (COUNT) {
@@ -1014,7 +1097,10 @@ struct rt_scene {
   const uint8_t *perlin = nullptr, *texels = nullptr;
   uint8_t* work = nullptr;  // per-sample radiance slots + f64 running sums (grown on demand)
   size_t work_bytes = 0;
-  unsigned long long* ops = nullptr;
+  unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
+  unsigned int* queue = nullptr;
+  int n_cu = 0;                 // compute units of the device
+  int resident_blocks[16] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;
 };
@@ -1079,7 +1165,9 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   sc->hdr = F.hdr;
   hipError_t e = hipMalloc(&sc->dev, total);
   if (e == hipSuccess) e = hipMemcpy(sc->dev, host.data(), total, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&sc->ops, sizeof(unsigned long long) * 32);
+  if (e == hipSuccess) e = hipMalloc(&sc->ops, sizeof(unsigned long long) * 32 + 256);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&sc->n_cu, hipDeviceAttributeMultiprocessorCount,
+                                                 device);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
   if (e != hipSuccess) {
@@ -1087,6 +1175,7 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
     return set_err(RT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
   }
   sc->dev_bytes = total;
+  sc->queue = (unsigned int*)(sc->ops + 32);
   sc->nodes = (const uint32_t*)(sc->dev + o_nodes);
   sc->mats = (const uint32_t*)(sc->dev + o_mats);
   sc->texs = (const uint32_t*)(sc->dev + o_texs);
@@ -1168,6 +1257,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.texels = sc->texels;
   P.samp = samp;
   P.ops = sc->ops;
+  P.queue = sc->queue;
   P.root = sc->hdr.root;
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
@@ -1217,12 +1307,27 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       rt_trace<true, false, true, false>,   rt_trace<true, false, true, true>,
       rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
       rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
-  kern_t kern = table[((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) + (uni ? 1 : 0)];
+  const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
+                   (uni ? 1 : 0);
+  kern_t kern = table[kidx];
+  if (sc->resident_blocks[kidx] == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kBlock, 0) !=
+            hipSuccess ||
+        nb <= 0)
+      nb = 1;
+    sc->resident_blocks[kidx] = nb;
+  }
+  const int64_t max_blocks = (int64_t)sc->resident_blocks[kidx] * std::max(1, sc->n_cu);
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
     const int cn = std::min(chunk, sj0 + n_sj - c0);
     P.sj0 = c0;
     P.n_sj = cn;
-    const int64_t blocks = (waves_per_sj * cn + (kBlock / 64) - 1) / (kBlock / 64);
+    P.n_pools = (int)(waves_per_sj * cn);
+    // persistent grid: as many waves as the device holds at once (never more than pools)
+    const int64_t blocks =
+        std::min(max_blocks, (waves_per_sj * cn + (kBlock / 64) - 1) / (kBlock / 64));
+    HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
     HIP_TRY(hipGetLastError());
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |

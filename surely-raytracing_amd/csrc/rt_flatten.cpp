@@ -165,13 +165,41 @@ struct Emitter {
     const double B[3] = {wv[1] * u[2] - wv[2] * u[1], wv[2] * u[0] - wv[0] * u[2],
                          wv[0] * u[1] - wv[1] * u[0]};
     w[p + 2] = (uint32_t)(n.mat < 0 ? 0 : n.mat);
-    putd(w, p, 0, f[9]), putd(w, p, 1, f[10]), putd(w, p, 2, f[11]), putd(w, p, 3, f[15]);
-    putd(w, p, 4, f[0]), putd(w, p, 5, f[1]), putd(w, p, 6, f[2]), putd(w, p, 7, f[16]);
-    putd(w, p, 8, A[0]), putd(w, p, 9, A[1]), putd(w, p, 10, A[2]);
-    putd(w, p, 12, B[0]), putd(w, p, 13, B[1]), putd(w, p, 14, B[2]);
+    const int g = light ? 0 : 6;  // general payload: d0 of a light record, d6 of a world record
+    putd(w, p, g + 0, f[9]), putd(w, p, g + 1, f[10]), putd(w, p, g + 2, f[11]);
+    putd(w, p, g + 3, f[15]);
+    putd(w, p, g + 4, f[0]), putd(w, p, g + 5, f[1]), putd(w, p, g + 6, f[2]);
+    putd(w, p, g + 7, f[16]);
+    putd(w, p, g + 8, A[0]), putd(w, p, g + 9, A[1]), putd(w, p, g + 10, A[2]);
+    putd(w, p, g + 12, B[0]), putd(w, p, g + 13, B[1]), putd(w, p, g + 14, B[2]);
     if (light) {
       putd(w, p, 16, u[0]), putd(w, p, 17, u[1]), putd(w, p, 18, u[2]);
       putd(w, p, 20, v[0]), putd(w, p, 21, v[1]), putd(w, p, 22, v[2]);
+      return;
+    }
+    // axis-aligned fast form (rt_layout.h): only when the exact-zero pattern holds
+    auto single = [](const double* x) {
+      int nz = -1;
+      for (int c = 0; c < 3; ++c)
+        if (x[c] != 0.0) {
+          if (nz >= 0) return -1;
+          nz = c;
+        }
+      return nz;
+    };
+    const int i = single(u), j = single(v);
+    if (i < 0 || j < 0 || i == j) return;
+    const int k = 3 - i - j;
+    const double nk = f[9 + k];
+    if (!(nk == 1.0 || nk == -1.0) || f[9 + i] != 0.0 || f[9 + j] != 0.0) return;
+    if (f[15] != nk * f[k]) return;  // D = n.q = n_k q_k
+    if (single(A) != i || single(B) != j) return;
+    w[p] |= (uint32_t)(k + 1) << 8;
+    putd(w, p, 0, f[k]);
+    if (i < j) {
+      putd(w, p, 1, f[i]), putd(w, p, 2, A[i]), putd(w, p, 3, f[j]), putd(w, p, 4, B[j]);
+    } else {
+      putd(w, p, 1, f[j]), putd(w, p, 2, B[j]), putd(w, p, 3, f[i]), putd(w, p, 4, A[i]);
     }
   }
   void sphere(const Node& n, bool light) {
@@ -401,6 +429,11 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
         o[0] = (uint32_t)kind;
         setd(o, 3, rd_f(b + 1));
         setd(o, 0, rd_f(b + 2)), setd(o, 1, rd_f(b + 3)), setd(o, 2, rd_f(b + 4));
+        {
+          const double ir = rd_f(b + 1), inv = 1.0 / ir;
+          const double rf = (1.0 - inv) / (1.0 + inv), rb = (1.0 - ir) / (1.0 + ir);
+          setd(o, 4, inv), setd(o, 5, rf * rf), setd(o, 6, rb * rb);
+        }
         break;
       default:
         *err = "unknown material kind";

@@ -39,7 +39,19 @@
  *   two dots per test).                                                  object.rs:414-490
  * Light records (LQUAD, 52 words) append d16-19 u.xyz,0 and d20-23 v.xyz,0 for Quad::random
  * (object.rs:503-506). */
-#define RTL_QUAD_WORDS 36
+/* World QUAD records (48 words) put an axis-aligned form FIRST, so one 64-byte scalar load
+ * covers the header and everything the axis-aligned test reads, and the general payload after it:
+ *   [hdr | axis << 8][skip][mat][0] d0-5 q_k, q_lo, C_lo, q_hi, C_hi, 0 | d6-21 general payload
+ * (the QUAD layout above, read through X + RTL_QUAD_GEN). axis = k + 1 when the quad is
+ * axis-aligned in its frame (u along axis i, v along axis j, normal along k; 0 = general). Then
+ * n = +-e_k, D = +-q_k, and A, B each have one non-zero component, so the general test's
+ *   t = (D - n.o) / (n.d) = (q_k - o_k) / d_k,   a = pq.A = pq_i A_i,   b = pq.B = pq_j B_j
+ * hold bit for bit (the dropped terms are exact zeros). lo/hi = the in-plane axes in ascending
+ * order, (q, C) = (q_i, A_i) or (q_j, B_j) accordingly: the accept test on (a, b) is symmetric,
+ * so only k varies per record. rt_flatten.cpp verifies the zero pattern before setting it. */
+#define RTL_QUAD_GEN 12
+#define RTL_QUAD_WORDS 48
+#define RTL_QUAD_AXIS(h) (((h) >> 8) & 0x3u)
 #define RTL_LQUAD_WORDS 52
 /* SPHERE (20 words): [hdr][skip][mat][moving] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r  object.rs:73-105 */
 #define RTL_SPHERE_WORDS 20
@@ -57,9 +69,12 @@
 #define RTL_VOLUME_WORDS 8
 #define RTL_END_WORDS 4
 
-/* material (12 words): [kind | flags(bit8: texture reads uv)][tex][0][0] d0-3 c.xyz, param
- *   METAL: c = albedo, param = fuzz; DIELECTRIC: c = tint, param = ir */
-#define RTL_MAT_WORDS 12
+/* material (20 words): [kind | flags(bit8: texture reads uv)][tex][0][0] d0-3 c.xyz, param,
+ * d4-7 derived constants
+ *   METAL: c = albedo, param = fuzz; DIELECTRIC: c = tint, param = ir, d4 = 1/ir,
+ *   d5 / d6 = Schlick r0 for the front / back face ratio (material.rs:150-158, 166-191; the same
+ *   IEEE divisions the reference performs per hit, done once on the host) */
+#define RTL_MAT_WORDS 20
 #define RTL_MATF_NEEDS_UV 0x100u
 /* texture (12 words): [kind][a][b][c] d0-3
  *   SOLID: d0-2 color; CHECKER: d0 inv_scale, a even, b odd;

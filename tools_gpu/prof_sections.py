@@ -23,5 +23,7 @@ for rep in range(2):
     assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
 cyc = np.array([st.ops[k] for k in range(8)], dtype=np.float64)
 print(f"{scene} {W} spp {cam.samples_per_pixel}: kernel {st.ms_kernel:.2f} ms (profiling build)")
+print(f"  lanes alive at traversal: {st.ops[8] / max(1, st.ops[9]):.2f} of 64 "
+      f"({st.ops[9]} wave-iterations)")
 for n, c in zip(NAMES, cyc):
     print(f"  {n:24s} {100 * c / cyc.sum():6.2f} %   {c / st.samples:9.1f} wave-cyc/sample")
