@@ -12,7 +12,9 @@ op-count pass are outside the timed region. value = W*H*spp_eff*steps / max-over
 
 Also reported (one JSON line on rank 0):
   roofline     FP64 VALU roofline of rt_trace: counted algorithmic flops per launch / the
-               kernel's average duration (torch.cuda.Event on the launch stream), vs 78.6 TF.
+               kernel's average duration (HIP events recorded by the library around each
+               rt_trace launch on the bench stream, rt_scene_trace_ms), vs 78.6 TF; render_ms =
+               the whole render call (rt_trace + rt_reduce, torch.cuda.Event on that stream).
   scene_fetch  the north star's "HBM GB/s on BVH traversal": logical scene-record bytes / time.
   cpu_baseline the f64 CPU oracle (a restatement of the reference; the Rust original cannot be
                built here) on this host's cores, timed on a bounded stratum subset of the same
@@ -148,7 +150,11 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(1, args.steps)
+    step_gpu_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(1, args.steps)
+    # the roofline's kernel: rt_trace alone (HIP events the library records around its launches
+    # on this stream), excluding the per-pixel reduction that step_gpu_ms also contains
+    trace = ds.trace_ms(args.steps)
+    kernel_ms = sum(trace) / max(1, len(trace))
 
     if rank == 0:
         total = W * H * spp * args.steps
@@ -191,6 +197,7 @@ def main():
                 "frac": round(ach / roofline.PEAK_FP64_VECTOR_TFLOPS, 4),
                 "traffic": traffic,
                 "kernel": "rt_trace", "kernel_ms": round(kernel_ms, 3),
+                "render_ms": round(step_gpu_ms, 3),
                 "flops_per_launch": fl, "flops_per_sample": round(fl / ops["samples"], 1),
             }
             gbps = by / (kernel_ms * 1e-3) / 1e9

@@ -194,7 +194,7 @@ int rt_device_count(int* count);
 /* Validate a blob without touching a device (hittable/object invariants, tag and index ranges). */
 int rt_scene_validate(const rt_scene_blob* blob);
 
-/* Validate, flatten (threaded node array, f32) and upload to `device`. */
+/* Validate, flatten (threaded node array, f64 payloads; rt_layout.h) and upload to `device`. */
 int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* scene);
 /* Bytes of the device-side flattened scene (nodes + materials + textures + tables). */
@@ -208,6 +208,13 @@ int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
  * If stats != NULL the call synchronises the stream to fill it. */
 int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
                      float* accum_rgb_device, void* hip_stream, rt_stats* stats);
+
+/* Device time (ms) of the path-tracing kernel alone (rt_trace, every chunk of one render summed;
+ * HIP events recorded on the render stream around its launches) for the most recent renders
+ * of `scene`, oldest first: up to max_n values, *n_out = count. Waits for those events. Used by
+ * the benchmark's roofline so the figure excludes the per-pixel reduction. */
+#define RT_TRACE_HISTORY 64
+int rt_scene_trace_ms(rt_scene* scene, float* ms_out, int max_n, int* n_out);
 
 /* One-shot drop-in for render_par_lights: create + render + destroy. */
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,

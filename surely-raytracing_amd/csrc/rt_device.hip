@@ -1102,6 +1102,11 @@ struct rt_scene {
   int n_cu = 0;                 // compute units of the device
   int resident_blocks[16] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
+  static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
+  hipEvent_t tev[kTraceRing][2] = {};
+  uint64_t tev_render[kTraceRing] = {};
+  uint64_t n_tev = 0, n_render = 0;
   std::mutex mu;
 };
 
@@ -1170,6 +1175,10 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
                                                  device);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
+  for (int k = 0; k < rt_scene::kTraceRing && e == hipSuccess; ++k) {
+    e = hipEventCreate(&sc->tev[k][0]);
+    if (e == hipSuccess) e = hipEventCreate(&sc->tev[k][1]);
+  }
   if (e != hipSuccess) {
     rt_scene_destroy(sc);
     return set_err(RT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
@@ -1195,6 +1204,9 @@ void rt_scene_destroy(rt_scene* sc) {
   if (sc->ops) (void)hipFree(sc->ops);
   if (sc->ev0) (void)hipEventDestroy(sc->ev0);
   if (sc->ev1) (void)hipEventDestroy(sc->ev1);
+  for (int k = 0; k < rt_scene::kTraceRing; ++k)
+    for (int j = 0; j < 2; ++j)
+      if (sc->tev[k][j]) (void)hipEventDestroy(sc->tev[k][j]);
   delete sc;
 }
 
@@ -1328,14 +1340,20 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     const int64_t blocks =
         std::min(max_blocks, (waves_per_sj * cn + (kBlock / 64) - 1) / (kBlock / 64));
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
+    const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
+    HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sc->tev[ring][1], stream));
+    sc->tev_render[ring] = sc->n_render;
+    ++sc->n_tev;
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
                      ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
     hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, stream, samp,
                        tot, accum, W, opts->n_rows, P.tiles_x, cn, S, mode);
     HIP_TRY(hipGetLastError());
   }
+  ++sc->n_render;
   if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));
   if (stats) {
     HIP_TRY(hipStreamSynchronize(stream));
@@ -1351,6 +1369,31 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     stats->ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  return RT_OK;
+}
+
+int rt_scene_trace_ms(rt_scene* sc, float* ms_out, int max_n, int* n_out) {
+  if (!sc || !ms_out || !n_out || max_n < 0) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lock(sc->mu);
+  HIP_TRY(hipSetDevice(sc->device));
+  const uint64_t R = rt_scene::kTraceRing;
+  const uint64_t first = sc->n_tev > R ? sc->n_tev - R : 0;
+  // a render whose first launches fell out of the ring is incomplete: skip it
+  const uint64_t skip_render = sc->n_tev > R ? sc->tev_render[first % R] : UINT64_MAX;
+  std::vector<std::pair<uint64_t, double>> per;  // (render id, ms), oldest first
+  for (uint64_t i = first; i < sc->n_tev; ++i) {
+    const int k = (int)(i % R);
+    const uint64_t id = sc->tev_render[k];
+    if (id == skip_render) continue;
+    HIP_TRY(hipEventSynchronize(sc->tev[k][1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, sc->tev[k][0], sc->tev[k][1]));
+    if (per.empty() || per.back().first != id) per.push_back({id, 0.0});
+    per.back().second += ms;
+  }
+  const int n = (int)std::min<size_t>((size_t)max_n, per.size());
+  for (int i = 0; i < n; ++i) ms_out[i] = (float)per[per.size() - n + i].second;
+  *n_out = n;
   return RT_OK;
 }
 

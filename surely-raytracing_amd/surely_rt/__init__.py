@@ -183,6 +183,8 @@ def load_device_lib(path: Path) -> C.CDLL:
         "rt_render_blob": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
                                      C.POINTER(RtRenderOpts), C.c_void_p,
                                      C.POINTER(RtStats)]),
+        "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
+                                        C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -445,6 +447,13 @@ class DeviceScene:
                                               C.c_void_p(dev_ptr), C.c_void_p(stream or None),
                                               C.byref(st) if st is not None else None))
         return st
+
+    def trace_ms(self, n: int) -> list[float]:
+        """Device ms of the rt_trace kernel alone for the last n renders (oldest first)."""
+        buf = (C.c_float * max(1, n))()
+        got = C.c_int(0)
+        _check_dev(self._lib.rt_scene_trace_ms(self._h, buf, n, C.byref(got)))
+        return [float(buf[i]) for i in range(got.value)]
 
 
 def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,

@@ -204,3 +204,16 @@ def test_c2_full_size_properties(gpu_available):
     assert np.array_equal(part, full[1::4])
     rgb = rt.write_color(full, cam.samples_per_pixel)
     assert abs(rgb.reshape(-1, 3).mean(0)[0] - 79.55) < 1.5
+
+
+def test_trace_kernel_timing_history(gpu_available):
+    """rt_scene_trace_ms reports the rt_trace launches of the last renders (one value per render,
+    chunks summed), each within the render's own device time."""
+    blob, cam = rt.preset_blob("cornell_box", width=96, spp=16)
+    ds = rt.DeviceScene(blob)
+    sts = [ds.render(cam, rt.make_opts(cam, seed=s))[1] for s in (1, 2, 3)]
+    ms = ds.trace_ms(8)
+    assert len(ms) == 3
+    for t, st in zip(ms, sts):
+        assert 0.0 < t <= st.ms_kernel + 1e-3
+    assert ds.trace_ms(2) == ms[1:]
