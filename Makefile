@@ -55,6 +55,13 @@ variants: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so
 	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so
 
+# occupancy variants of the BVH kernels; A/B with
+# VARDIR=build/variants_occ python tools_gpu/ab_variants.py W SPP ROUNDS SCENE
+variants-occ: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_occ
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=3 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh3.so
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=4 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh4.so
+
 # section-cycle profiling build (tools_gpu/prof_sections.py); not shipped
 prof: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/prof

@@ -34,6 +34,13 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "surely-raytracing_amd"))
 
 METRIC = "Msamples/sec (pixels*spp/s), Cornell box 800x800 @ 1/2/4/8 MI355X"
+# BASELINE.json configs that fit one GPU. c2 is the headline the metric is quoted on;
+# c3/c4 use the same harness (their lines are reported under the same unit, tagged by workload).
+CONFIGS = {
+    "c2": dict(name="BASELINE configs[1]", scene="cornell_box", width=800, spp=1000, depth=50),
+    "c3": dict(name="BASELINE configs[2]", scene="cornell_smoke", width=800, spp=1000, depth=10),
+    "c4": dict(name="BASELINE configs[3]", scene="final_scene", width=800, spp=5000, depth=40),
+}
 
 
 def parse():
@@ -41,16 +48,25 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="cornell_box")
-    ap.add_argument("--width", type=int, default=800)
-    ap.add_argument("--spp", type=int, default=1000)
-    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE config (c2 = the headline; c3/c4 = the other 1-GPU configs)")
+    ap.add_argument("--scene", default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU-baseline work (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the op-count pass")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    for k in ("scene", "width", "spp", "depth"):
+        if getattr(a, k) is None:
+            setattr(a, k, c[k])
+    a.config_name = c["name"] if (a.scene, a.width, a.spp, a.depth) == (
+        c["scene"], c["width"], c["spp"], c["depth"]) else "custom"
+    return a
 
 
 def cpu_baseline(blob, cam, seed, target_s):
@@ -174,7 +190,7 @@ def main():
             "data": "synthetic (procedural reference scene, no input data)",
             "config": {
                 "workload": f"{args.scene} {W}x{H}, {args.spp}->{spp} spp, depth {cam.max_depth}"
-                            " (BASELINE configs[1])",
+                            f" ({args.config_name})",
                 "width": W, "height": H, "spp_effective": spp, "max_depth": cam.max_depth,
                 "seed": args.seed, "parallelism": f"cyclic rows x{world}, gather to rank 0",
             },
@@ -184,9 +200,11 @@ def main():
             fl = roofline.flops(ops)
             by = roofline.scene_bytes(ops, partial_bytes=n * W * spp * 24)  # sample slots w+r
             ach = fl / (kernel_ms * 1e-3) / 1e12
+            # PMC HBM bytes per rt_trace launch, measured by tools_gpu/profile_round.sh at N = 1
+            # for this exact workload (null otherwise: a rank's launch at N > 1 is a different size)
             traffic = None
-            tf = REPO / "profiles" / "pmc_traffic.json"
-            if tf.exists():
+            tf = REPO / "profiles" / f"pmc_traffic_{args.config}.json"
+            if world == 1 and args.config_name != "custom" and tf.exists():
                 try:
                     traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
                 except Exception:

@@ -45,11 +45,21 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 constexpr int kBlock = 256;   // 4 waves per workgroup
-// Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument): 4 caps the
-// allocation at 128 VGPRs (tools_gpu/ab_variants.py measures the trade against spills).
+// Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument). 4 caps the
+// allocation at 128 VGPRs. Kernels with a per-lane BVH walker need more than that without
+// spilling inside the walk, and spills there cost more than the occupancy they buy: 2 waves
+// (256 VGPRs) measured 294 vs 214 Msamples/s on final_scene; volume/texture kernels without a
+// BVH stay at 4 (cornell_smoke: 2221 at 4 vs 1985 at 2). tools_gpu/ab_variants.py, variants-occ.
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 4
 #endif
+#ifndef RT_MIN_WAVES_BVH
+#define RT_MIN_WAVES_BVH 2
+#endif
+template <bool VOL, bool TEX, bool BVH>
+struct MinWaves {
+  static constexpr int value = BVH ? RT_MIN_WAVES_BVH : RT_MIN_WAVES;
+};
 
 struct d3 {
   double x, y, z;
@@ -143,6 +153,10 @@ __device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
   *co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
 }
 
+// Perlin tables staged per workgroup (dynamic LDS of the TEX kernels: n_perlin_lds tables)
+constexpr uint32_t kPerlinLds = 4;
+extern __shared__ __attribute__((aligned(16))) uint8_t rt_lds_perlin[];
+
 struct TraceParams {
   const uint32_t* __restrict__ nodes;
   const uint32_t* __restrict__ mats;
@@ -156,6 +170,7 @@ struct TraceParams {
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
   int n_pools;                       // pools of this launch: tiles x n_sj
   uint32_t root, n_lights, lights_is_list, flags;
+  uint32_t n_perlin_lds;  // Perlin tables copied into LDS at launch (TEX kernels)
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
   int defocus;
@@ -206,6 +221,14 @@ __device__ __forceinline__ double ldd(gptr X, int k) {
 __device__ __forceinline__ double ldd(kptr X, int k) { return reinterpret_cast<kdptr>(X + 4)[k]; }
 __device__ __forceinline__ uint4 ld4u(gptr p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ uint4 ld4u(kptr p) { return make_uint4(p[0], p[1], p[2], p[3]); }
+// first 64 bytes of a node record: four independent 16-byte loads, one memory round trip
+template <class Ptr>
+__device__ __forceinline__ void ld64(Ptr p, uint4& a, uint4& b, uint4& c, uint4& e) {
+  a = ld4u(p);
+  b = ld4u(p + 4);
+  c = ld4u(p + 8);
+  e = ld4u(p + 12);
+}
 __device__ __forceinline__ d3 arr3(const double* a) { return mk(a[0], a[1], a[2]); }
 
 // ---------------------------------------------------------------- op counters (COUNT build)
@@ -309,6 +332,20 @@ __device__ __forceinline__ bool world_quad_test(Ptr Q, d3 o, d3 d, d3 r, double 
   }
 }
 
+// world_quad_test on an axis-aligned form already in registers (Q = the record, for the
+// general payload of a non-axis-aligned quad).
+template <bool COUNT, class Ptr>
+__device__ __forceinline__ bool aquad_dispatch(const AQuad& q, Ptr Q, d3 o, d3 d, d3 r,
+                                               double tmin, double tmax, double& t_out,
+                                               Ctr<COUNT>& C) {
+  switch (RTL_QUAD_AXIS(q.h0)) {
+    case 1u: return aquad_test<COUNT, 0>(q, o, d, r, tmin, tmax, t_out, C);
+    case 2u: return aquad_test<COUNT, 1>(q, o, d, r, tmin, tmax, t_out, C);
+    case 3u: return aquad_test<COUNT, 2>(q, o, d, r, tmin, tmax, t_out, C);
+    default: return quad_test<COUNT>(Q + RTL_QUAD_GEN, o, d, tmin, tmax, t_out, C);
+  }
+}
+
 // Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
 template <bool COUNT, class Ptr>
 __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double tmin,
@@ -336,11 +373,10 @@ __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double
   return true;
 }
 
-// Aabb::hit object.rs:340-370 with inv_d = 1/d computed once per ray frame.
-template <class Ptr>
-__device__ __forceinline__ bool aabb_test(Ptr b, d3 o, d3 inv, double tmin, double tmax) {
-  const double mn[3] = {ldd(b, 0), ldd(b, 2), ldd(b, 4)};
-  const double mx[3] = {ldd(b, 1), ldd(b, 3), ldd(b, 5)};
+// Aabb::hit object.rs:340-370 on bounds already in registers (the LANE walker's 64-byte node
+// fetch), with inv_d = 1/d computed once per ray frame.
+__device__ __forceinline__ bool aabb_hit(const double (&mn)[3], const double (&mx)[3], d3 o,
+                                         d3 inv, double tmin, double tmax) {
   const double oo[3] = {o.x, o.y, o.z}, id[3] = {inv.x, inv.y, inv.z};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -396,12 +432,22 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
 // ---------------------------------------------------------------- traversal
 // Threaded walk of the flattened scene (rt_layout.h). MAIN: the world (records the hit node and
 // its frame, handles ConstantMedium when VOL). !MAIN: a volume boundary (closest t only).
-// UNI: the scene has no BVH, so the node sequence is the same for every lane and the node
-// index is kept wave-uniform (scalar loads). Otherwise each lane follows its own skips.
-template <bool MAIN, bool COUNT, bool VOL, bool UNI>
-__device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, double tm, d3 o, d3 d,
-                         int frame, double tmin, double tmax, double& t_out, uint32_t& hit_node,
-                         int& hit_frame, Rng& g, Ctr<COUNT>& C) {
+//
+// Two walkers share this body:
+//  UNI  (wave-uniform): outside BVH subtrees the node sequence does not depend on the ray (lists,
+//       transforms, volumes and primitives are visited in a fixed order), so the node index is
+//       readfirstlane'd and node records arrive by scalar loads (K$, SGPRs, no VGPRs). Used for
+//       every scene's top level.
+//  LANE (per-lane): inside a BVH subtree each lane follows its own skip links. Each node's first
+//       64 bytes (header + bbox, or header + axis-aligned quad form) are fetched by four
+//       independent 16-byte vector loads, so one memory round trip serves a BVH node. The UNI
+//       walker hands a BVH subtree [root, skip) to the LANE walker with the current closest-hit
+//       state and resumes at its skip once every lane has finished it (BVH = the scene has one).
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH>
+__device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
+                         double tm, d3 o, d3 d, int frame, double tmin, double tmax,
+                         double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
+                         Ctr<COUNT>& C) {
   typedef typename std::conditional<UNI, kptr, gptr>::type Ptr;
   const Ptr N = (Ptr)P.nodes;
   double closest = tmax;
@@ -409,17 +455,46 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
   d3 inv = mk(0., 0., 0.);
   bool inv_ok = false;
   for (;;) {
+    uint4 h, q1, q2, q3;
     if (UNI) {
       node = __builtin_amdgcn_readfirstlane(node);
       frame = __builtin_amdgcn_readfirstlane(frame);
+      h = ld4u(N + node);
+    } else {
+      if (node == stop) break;
+      // speculative 64-byte fetch (the node array is padded past its END)
+      ld64(N + node, h, q1, q2, q3);
+      // while-while: a lane steps through BVH nodes until it reaches a leaf (or the subtree's
+      // end); lanes that got there first wait at the loop exit, so the leaf bodies below run
+      // with every lane that has a leaf instead of interleaving with the AABB steps.
+      while ((h.x & 0xffu) == RTL_BVH) {
+        C.inc(RT_OP_AABB_TESTS);
+        if (!inv_ok) {
+          inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+          inv_ok = true;
+        }
+        const double mn[3] = {hilo(q1.x, q1.y), hilo(q2.x, q2.y), hilo(q3.x, q3.y)};
+        const double mx[3] = {hilo(q1.z, q1.w), hilo(q2.z, q2.w), hilo(q3.z, q3.w)};
+        node = aabb_hit(mn, mx, o, inv, tmin, closest) ? node + RTL_BVH_WORDS : h.y;
+        if (node == stop) break;
+        ld64(N + node, h, q1, q2, q3);
+      }
+      if (node == stop) break;
     }
     const Ptr X = N + node;
-    uint4 h = ld4u(X);
     uint32_t type = h.x & 0xffu;
     if (type == RTL_QUAD) {
       double t;
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
-      if (world_quad_test<COUNT>(X, o, d, r, tmin, closest, t, C)) {
+      bool hq;
+      if (UNI) {
+        hq = world_quad_test<COUNT>(X, o, d, r, tmin, closest, t, C);
+      } else {
+        const AQuad q = {h.x, hilo(q1.x, q1.y), hilo(q1.z, q1.w), hilo(q2.x, q2.y),
+                         hilo(q2.z, q2.w), hilo(q3.x, q3.y)};
+        hq = aquad_dispatch<COUNT>(q, X, o, d, r, tmin, closest, t, C);
+      }
+      if (hq) {
         closest = t;
         hit = true;
         if (MAIN) {
@@ -433,9 +508,20 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
       const uint32_t cnt = h.x >> 8;
       Ptr Q = X + 4;
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+      uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
+      if (!UNI) ld64(Q, a0, a1, a2, a3);
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
         double t;
-        if (world_quad_test<COUNT>(Q, o, d, r, tmin, closest, t, C)) {
+        bool hq;
+        if (UNI) {
+          hq = world_quad_test<COUNT>(Q, o, d, r, tmin, closest, t, C);
+        } else {
+          const AQuad q = {a0.x, hilo(a1.x, a1.y), hilo(a1.z, a1.w), hilo(a2.x, a2.y),
+                           hilo(a2.z, a2.w), hilo(a3.x, a3.y)};
+          ld64(Q + RTL_QUAD_WORDS, a0, a1, a2, a3);  // past the batch: the next node (padded)
+          hq = aquad_dispatch<COUNT>(q, Q, o, d, r, tmin, closest, t, C);
+        }
+        if (hq) {
           closest = t;
           hit = true;
           if (MAIN) {
@@ -457,12 +543,23 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
       }
       node += RTL_SPHERE_WORDS;
     } else if (type == RTL_BVH) {
-      C.inc(RT_OP_AABB_TESTS);
-      if (!inv_ok) {
-        inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-        inv_ok = true;
-      }
-      node = aabb_test(X, o, inv, tmin, closest) ? node + RTL_BVH_WORDS : h.y;
+      if (UNI) {
+        if (BVH) {  // the subtree [node, skip) per lane, continuing this walk's closest hit
+          double t;
+          uint32_t hn;
+          int hf;
+          if (traverse<MAIN, COUNT, VOL, false, BVH>(P, node, h.y, wo, wd, tm, o, d, frame, tmin,
+                                                     closest, t, hn, hf, g, C)) {
+            closest = t;
+            hit = true;
+            if (MAIN) {
+              hit_node = hn;
+              hit_frame = hf;
+            }
+          }
+        }
+        node = h.y;
+      }  // LANE: BVH nodes never get here (the while-while step above consumes them)
     } else if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y) {
       C.inc(type == RTL_TRANSLATE ? RT_OP_TRANSLATE : RT_OP_ROTATE_Y);
       xform_in(X, o, d);
@@ -477,13 +574,22 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, d3 wo, d3 wd, doub
     } else if (MAIN && VOL && type == RTL_VOLUME) {
       // ConstantMedium::hit constant_medium.rs:41-95
       C.inc(RT_OP_VOLUME_TESTS);
-      double t1, t2;
-      uint32_t dn;
-      int df;
-      if (traverse<false, COUNT, false, UNI>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
-                                        -INFINITY, INFINITY, t1, dn, df, g, C) &&
-          traverse<false, COUNT, false, UNI>(P, node + RTL_VOLUME_WORDS, wo, wd, tm, o, d, frame,
-                                        t1 + 0.0001, INFINITY, t2, dn, df, g, C)) {
+      // rec1 = boundary.hit(r, (-inf, inf)), rec2 = boundary.hit(r, [rec1.t + 1e-4, inf)):
+      // one rolled loop, so the boundary walker is instantiated once
+      double t1 = 0.0, t2 = 0.0;
+      bool both = true;
+#pragma unroll 1
+      for (int pass = 0; pass < 2 && both; ++pass) {
+        double tb;
+        uint32_t dn;
+        int df;
+        both = traverse<false, COUNT, false, UNI, BVH>(P, node + RTL_VOLUME_WORDS, ~0u, wo, wd, tm,
+                                                       o, d, frame,
+                                                       pass ? t1 + 0.0001 : -INFINITY, INFINITY,
+                                                       tb, dn, df, g, C);
+        if (pass) t2 = tb; else t1 = tb;
+      }
+      if (both) {
         if (t1 < tmin) t1 = tmin;
         if (t2 > closest) t2 = closest;
         if (t1 < t2) {
@@ -524,18 +630,25 @@ __device__ __forceinline__ uint32_t f2u_sat(double f) {  // Rust `as u32`
   return (uint32_t)f;
 }
 
-// Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96 (out of line: only
-// noise-textured materials reach it)
-__device__ __noinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) {
+// Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96. T = one table
+// (RTL_PERLIN_BYTES: ranvec as 256 double4, then perm_x/y/z), normally the workgroup's LDS copy
+// (rt_trace stages the scene's first kPerlinLds tables at launch). The octave loop stays rolled
+// and each octave reads the six permutation entries once, so the eight corner gathers are the
+// only wide live values.
+__device__ __forceinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) {
   const double* rv = reinterpret_cast<const double*>(T);
   const uint8_t* px = T + 8192;
   const uint8_t* py = px + 256;
   const uint8_t* pz = py + 256;
   double accum = 0.0, weight = 1.0;
+#pragma unroll 1
   for (int oct = 0; oct < 7; ++oct) {
     double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
     double u = p.x - fx, v = p.y - fy, w = p.z - fz;
-    int32_t i = f2i_sat(fx), j = f2i_sat(fy), k = f2i_sat(fz);
+    const uint32_t i = (uint32_t)f2i_sat(fx), j = (uint32_t)f2i_sat(fy), k = (uint32_t)f2i_sat(fz);
+    const uint32_t X[2] = {px[i & 255u], px[(i + 1u) & 255u]};
+    const uint32_t Y[2] = {py[j & 255u], py[(j + 1u) & 255u]};
+    const uint32_t Z[2] = {pz[k & 255u], pz[(k + 1u) & 255u]};
     double uu = u * u * (3.0 - 2.0 * u);
     double vv = v * v * (3.0 - 2.0 * v);
     double ww = w * w * (3.0 - 2.0 * w);
@@ -546,8 +659,7 @@ __device__ __noinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) 
       for (int dj = 0; dj < 2; ++dj)
 #pragma unroll
         for (int dk = 0; dk < 2; ++dk) {
-          uint32_t idx = px[(uint32_t)(i + di) & 255u] ^ py[(uint32_t)(j + dj) & 255u] ^
-                         pz[(uint32_t)(k + dk) & 255u];
+          const uint32_t idx = X[di] ^ Y[dj] ^ Z[dk];
           double2 cxy = *reinterpret_cast<const double2*>(rv + 4 * idx);
           d3 c = mk(cxy.x, cxy.y, rv[4 * idx + 2]);
           double wi = di ? uu : 1.0 - uu;
@@ -561,6 +673,10 @@ __device__ __noinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) 
     p = p * 2.0;
   }
   return fabs(accum);
+}
+// Tables past the LDS-staged ones (scenes with more than kPerlinLds noise textures): global.
+__device__ __noinline__ double perlin_turb_global(const uint8_t* __restrict__ T, d3 p) {
+  return perlin_turb(T, p);
 }
 
 template <bool COUNT, bool TEX>
@@ -597,7 +713,9 @@ __device__ d3 tex_value(const TraceParams& P, uint32_t id, double u, double v, d
     if (h.x == RT_TEX_NOISE) {  // texture.rs:127-130
       C.inc(RT_OP_NOISE_EVALS);
       d3 s = p * ldd(t, 0);
-      double turb = perlin_turb(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
+      double turb = h.y < P.n_perlin_lds
+                        ? perlin_turb(rt_lds_perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
+                        : perlin_turb_global(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
       double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
       return mk(k, k, k);
     }
@@ -683,11 +801,18 @@ __device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t sl
 
 // ---------------------------------------------------------------- the path kernel
 // VOL: scene has ConstantMedium nodes; TEX: some material reads a non-solid texture.
-template <bool COUNT, bool VOL, bool TEX, bool UNI>
-__global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) {
+template <bool COUNT, bool VOL, bool TEX, bool BVH>
+__global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(TraceParams P) {
   __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
   if (COUNT) {
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
+    __syncthreads();
+  }
+  if (TEX && P.n_perlin_lds) {  // stage the Perlin tables (perlin.rs:97-117 data) in LDS
+    const uint4* src = reinterpret_cast<const uint4*>(P.perlin);
+    uint4* dst = reinterpret_cast<uint4*>(rt_lds_perlin);
+    const uint32_t n16 = P.n_perlin_lds * (RTL_PERLIN_BYTES / 16);
+    for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
   }
   Ctr<COUNT> C;
@@ -830,13 +955,14 @@ __global__ __launch_bounds__(kBlock, RT_MIN_WAVES) void rt_trace(TraceParams P) 
       double t2;
       uint32_t hn2;
       int hf2;
-      traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001 + z, INFINITY, t2,
+      traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001 + z,
+                                            INFINITY, t2,
                                       hn2, hf2, g, C);
       asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
     }
 #endif
-    if (!traverse<true, COUNT, VOL, UNI>(P, P.root, ro, rd, tm, ro, rd, -1, 0.0001, INFINITY, t, hn,
-                                    hf, g, C)) {
+    if (!traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001,
+                                               INFINITY, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * karr3(kparams()->bg);
       store_sample(P.samp, slot, Lp);
@@ -1147,7 +1273,8 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   // pack tables into one 256-B aligned allocation
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t o_nodes = 0, s_nodes = F.nodes.size() * 4;
-  size_t o_mats = al(o_nodes + s_nodes), s_mats = F.mats.size() * 4;
+  // +64 B: the LANE walker fetches 64 bytes of every node it visits, END (16 B) included
+  size_t o_mats = al(o_nodes + s_nodes + 64), s_mats = F.mats.size() * 4;
   size_t o_texs = al(o_mats + s_mats), s_texs = F.texs.size() * 4;
   size_t o_perl = al(o_texs + s_texs), s_perl = F.perlin.size();
   size_t o_lig = al(o_perl + s_perl), s_lig = F.lights.size() * 4;
@@ -1274,6 +1401,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
   P.flags = opts->flags;
+  P.n_perlin_lds = sc->hdr.has_textures ? std::min<uint32_t>(sc->hdr.n_perlins, kPerlinLds) : 0u;
+  const size_t lds_bytes = (size_t)P.n_perlin_lds * RTL_PERLIN_BYTES;
   for (int k = 0; k < 3; ++k) {
     P.center[k] = cam->center[k];
     P.p00[k] = cam->pixel00_loc[k];
@@ -1307,9 +1436,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
   const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
-  const bool uni = sc->hdr.has_bvh == 0;
+  const bool bvh = sc->hdr.has_bvh != 0;
   typedef void (*kern_t)(TraceParams);
-  // [count][vol][tex][uni]
+  // [count][vol][tex][bvh]
   static const kern_t table[16] = {
       rt_trace<false, false, false, false>, rt_trace<false, false, false, true>,
       rt_trace<false, false, true, false>,  rt_trace<false, false, true, true>,
@@ -1320,11 +1449,11 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
       rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
-                   (uni ? 1 : 0);
+                   (bvh ? 1 : 0);
   kern_t kern = table[kidx];
   if (sc->resident_blocks[kidx] == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kBlock, lds_bytes) !=
             hipSuccess ||
         nb <= 0)
       nb = 1;
@@ -1342,7 +1471,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
     const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, stream, P);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), lds_bytes, stream, P);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sc->tev[ring][1], stream));
     sc->tev_render[ring] = sc->n_render;

@@ -2,6 +2,7 @@
 (cdna_hip_programming.md §5.4 rule 24). Usage: python tools_gpu/ab_variants.py [width spp rounds]"""
 import ctypes as C
 import glob
+import os
 import sys
 import time
 
@@ -13,7 +14,8 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 else 800
 SPP = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 ROUNDS = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 SCENE = sys.argv[4] if len(sys.argv) > 4 else "cornell_box"
-paths = ["build/librtmi355x.so"] + sorted(glob.glob("build/variants/*.so"))
+VARDIR = os.environ.get("VARDIR", "build/variants")
+paths = ["build/librtmi355x.so"] + sorted(glob.glob(f"{VARDIR}/*.so"))
 blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
 libs, scenes = [], []
 for p in paths:
