@@ -155,7 +155,17 @@ __device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
 
 // Perlin tables staged per workgroup (dynamic LDS of the TEX kernels: n_perlin_lds tables)
 constexpr uint32_t kPerlinLds = 4;
-extern __shared__ __attribute__((aligned(16))) uint8_t rt_lds_perlin[];
+// Scenes whose node/material/texture/light tables (+ Perlin tables) fit this many bytes are
+// staged in LDS whole: 4 workgroups per CU x 24 KiB stay well inside the CU's 160 KiB.
+constexpr size_t kStageScene = 24u << 10;
+extern __shared__ __attribute__((aligned(16))) uint8_t rt_lds[];
+
+// Table pointers for per-lane (divergent) reads: the workgroup's LDS copy of a small scene, or
+// the global tables. Generic pointers: the same code reads either.
+struct Tabs {
+  const uint32_t *nodes, *mats, *texs, *lights, *loffs;
+  const uint8_t* perlin;  // LDS: the staged Perlin tables
+};
 
 struct TraceParams {
   const uint32_t* __restrict__ nodes;
@@ -170,7 +180,14 @@ struct TraceParams {
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
   int n_pools;                       // pools of this launch: tiles x n_sj
   uint32_t root, n_lights, lights_is_list, flags;
-  uint32_t n_perlin_lds;  // Perlin tables copied into LDS at launch (TEX kernels)
+  uint32_t n_perlin_lds;  // Perlin tables readable from LDS (TEX kernels)
+  // LDS staging (rt_trace prologue): stage_bytes of the scene allocation starting at stage_src.
+  // stage_scene = 1: the whole small-table prefix [nodes .. Perlin] is copied, and per-lane
+  // (divergent) reads of nodes / materials / textures / lights use the copy; 0: only the first
+  // n_perlin_lds Perlin tables are copied. Offsets are bytes from the start of the allocation.
+  const uint8_t* stage_src;
+  uint32_t stage_bytes, stage_scene;
+  uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
   int defocus;
@@ -680,11 +697,11 @@ __device__ __noinline__ double perlin_turb_global(const uint8_t* __restrict__ T,
 }
 
 template <bool COUNT, bool TEX>
-__device__ d3 tex_value(const TraceParams& P, uint32_t id, double u, double v, d3 p,
-                        Ctr<COUNT>& C) {
-  if (!TEX) return ld3(P.texs + (size_t)id * RTL_TEX_WORDS, 0);
+__device__ d3 tex_value(const TraceParams& P, const Tabs& T, uint32_t id, double u, double v,
+                        d3 p, Ctr<COUNT>& C) {
+  if (!TEX) return ld3(T.texs + (size_t)id * RTL_TEX_WORDS, 0);
   for (int guard = 0; guard < 65; ++guard) {
-    const uint32_t* t = P.texs + (size_t)id * RTL_TEX_WORDS;
+    const uint32_t* t = T.texs + (size_t)id * RTL_TEX_WORDS;
     uint4 h = ld4u(t);
     if (h.x == RT_TEX_SOLID) return ld3(t, 0);
     if (h.x == RT_TEX_CHECKER) {  // texture.rs:71-81
@@ -714,7 +731,7 @@ __device__ d3 tex_value(const TraceParams& P, uint32_t id, double u, double v, d
       C.inc(RT_OP_NOISE_EVALS);
       d3 s = p * ldd(t, 0);
       double turb = h.y < P.n_perlin_lds
-                        ? perlin_turb(rt_lds_perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
+                        ? perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
                         : perlin_turb_global(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
       double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
       return mk(k, k, k);
@@ -808,12 +825,22 @@ __global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_t
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
     __syncthreads();
   }
-  if (TEX && P.n_perlin_lds) {  // stage the Perlin tables (perlin.rs:97-117 data) in LDS
-    const uint4* src = reinterpret_cast<const uint4*>(P.perlin);
-    uint4* dst = reinterpret_cast<uint4*>(rt_lds_perlin);
-    const uint32_t n16 = P.n_perlin_lds * (RTL_PERLIN_BYTES / 16);
+  if (P.stage_bytes) {  // copy the small tables (or just the Perlin tables) into LDS
+    const uint4* src = reinterpret_cast<const uint4*>(P.stage_src);
+    uint4* dst = reinterpret_cast<uint4*>(rt_lds);
+    const uint32_t n16 = P.stage_bytes / 16;
     for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
     __syncthreads();
+  }
+  Tabs T;
+  {
+    const uint8_t* b = P.stage_scene ? (const uint8_t*)rt_lds : (const uint8_t*)P.nodes;
+    T.nodes = reinterpret_cast<const uint32_t*>(b);
+    T.mats = reinterpret_cast<const uint32_t*>(b + P.o_mats);
+    T.texs = reinterpret_cast<const uint32_t*>(b + P.o_texs);
+    T.lights = reinterpret_cast<const uint32_t*>(b + P.o_lights);
+    T.loffs = reinterpret_cast<const uint32_t*>(b + P.o_loffs);
+    T.perlin = rt_lds + (P.stage_scene ? P.o_perl : 0u);
   }
   Ctr<COUNT> C;
 #ifdef RT_PROF  // profiling build: wave cycles per loop section into P.ops[0..7] (not shipped)
@@ -971,15 +998,15 @@ __global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_t
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
     PROF(2);
-    const uint32_t* X = P.nodes + hn;
+    const uint32_t* X = T.nodes + hn;
     uint32_t type = X[0] & 0xffu;
     d3 o, d;
-    frame_ray(P.nodes, hf, ro, rd, o, d);
+    frame_ray(T.nodes, hf, ro, rd, o, d);
     d3 p = vfma(t, d, o);
     d3 normal;
     bool front = true;
     double u = 0., v = 0.;
-    const uint32_t* M = P.mats + (size_t)X[2] * RTL_MAT_WORDS;
+    const uint32_t* M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
     uint4 mh = ld4u(M);
     const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
     if (type == RTL_QUAD) {
@@ -1003,18 +1030,18 @@ __global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_t
       normal = mk(1., 0., 0.);
     }
     if (hf >= 0) {  // back to world space, innermost transform first
-      uint4 fh = ld4u(P.nodes + hf);
-      uint4 ch = ld4u(P.nodes + hf + 4);
+      uint4 fh = ld4u(T.nodes + hf);
+      uint4 ch = ld4u(T.nodes + hf + 4);
       const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
 #pragma unroll
       for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
-        if ((uint32_t)k < fh.z) xform_out(P.nodes + c4[k], p, normal);
+        if ((uint32_t)k < fh.z) xform_out(T.nodes + c4[k], p, normal);
     }
     const uint32_t kind = mh.x & 0xffu;
     PROF(3);
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
-      if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, mh.y, u, v, p, C), Lp);
+      if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
       store_sample(P.samp, slot, Lp);
       alive = false;
       continue;
@@ -1053,17 +1080,17 @@ __global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_t
     PROF(4);
     const bool iso = kind == RT_MAT_ISOTROPIC;
     C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
-    d3 atten = tex_value<COUNT, TEX>(P, mh.y, u, v, p, C);
+    d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
     // Draw order as the reference: mixture coin (pdf.rs:120-126), then light index
     // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
     bool light_branch = false;
     if (have_lights) light_branch = rnd(g) < 0.5;
     uint32_t ltype = 0;
-    gptr L = P.lights;
+    gptr L = T.lights;
     if (light_branch) {
       C.inc(RT_OP_LIGHT_GEN);
       uint32_t li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
-      L = P.lights + P.light_offs[li];
+      L = T.lights + T.loffs[li];
       ltype = L[0] & 0xffu;
     } else {
       C.inc(RT_OP_COSINE_GEN);
@@ -1221,6 +1248,7 @@ struct rt_scene {
   const uint32_t *nodes = nullptr, *mats = nullptr, *texs = nullptr, *lights = nullptr,
                  *light_offs = nullptr;
   const uint8_t *perlin = nullptr, *texels = nullptr;
+  uint32_t o_mats = 0, o_texs = 0, o_lights = 0, o_loffs = 0, o_perl = 0;  // byte offsets in dev
   uint8_t* work = nullptr;  // per-sample radiance slots + f64 running sums (grown on demand)
   size_t work_bytes = 0;
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
@@ -1270,16 +1298,18 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
     return set_err(RT_ERR_NO_DEVICE, "no HIP device available");
   if (device < 0 || device >= ndev) return set_err(RT_ERR_INVALID_ARG, "bad device ordinal");
   HIP_TRY(hipSetDevice(device));
-  // pack tables into one 256-B aligned allocation
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  // Pack the tables into one allocation, in the order the kernel stages them into LDS (a
+  // prefix of it: nodes, materials, textures, lights, light offsets, Perlin tables), 16-byte
+  // aligned; texels last (never staged).
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t o_nodes = 0, s_nodes = F.nodes.size() * 4;
   // +64 B: the LANE walker fetches 64 bytes of every node it visits, END (16 B) included
   size_t o_mats = al(o_nodes + s_nodes + 64), s_mats = F.mats.size() * 4;
   size_t o_texs = al(o_mats + s_mats), s_texs = F.texs.size() * 4;
-  size_t o_perl = al(o_texs + s_texs), s_perl = F.perlin.size();
-  size_t o_lig = al(o_perl + s_perl), s_lig = F.lights.size() * 4;
+  size_t o_lig = al(o_texs + s_texs), s_lig = F.lights.size() * 4;
   size_t o_loff = al(o_lig + s_lig), s_loff = F.light_offs.size() * 4;
-  size_t o_tx = al(o_loff + s_loff), s_tx = F.texels.size();
+  size_t o_perl = al(o_loff + s_loff), s_perl = F.perlin.size();
+  size_t o_tx = al(o_perl + s_perl), s_tx = F.texels.size();
   size_t total = al(o_tx + s_tx) + 256;
   std::vector<uint8_t> host(total, 0);
   auto cp = [&](size_t off, const void* src, size_t n) {
@@ -1319,6 +1349,11 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   sc->lights = (const uint32_t*)(sc->dev + o_lig);
   sc->light_offs = (const uint32_t*)(sc->dev + o_loff);
   sc->texels = sc->dev + o_tx;
+  sc->o_mats = (uint32_t)o_mats;
+  sc->o_texs = (uint32_t)o_texs;
+  sc->o_lights = (uint32_t)o_lig;
+  sc->o_loffs = (uint32_t)o_loff;
+  sc->o_perl = (uint32_t)o_perl;
   *out = sc;
   return RT_OK;
 }
@@ -1401,8 +1436,26 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
   P.flags = opts->flags;
-  P.n_perlin_lds = sc->hdr.has_textures ? std::min<uint32_t>(sc->hdr.n_perlins, kPerlinLds) : 0u;
-  const size_t lds_bytes = (size_t)P.n_perlin_lds * RTL_PERLIN_BYTES;
+  // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
+  // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.
+  const uint32_t used_perlins = sc->hdr.has_textures ? sc->hdr.n_perlins : 0u;
+  const size_t scene_prefix = sc->o_perl + (size_t)used_perlins * RTL_PERLIN_BYTES;
+  P.stage_scene = scene_prefix <= kStageScene ? 1u : 0u;
+  if (P.stage_scene) {
+    P.n_perlin_lds = used_perlins;
+    P.stage_src = sc->dev;
+    P.stage_bytes = (uint32_t)((scene_prefix + 15) & ~(size_t)15);
+  } else {
+    P.n_perlin_lds = std::min<uint32_t>(used_perlins, kPerlinLds);
+    P.stage_src = sc->perlin;
+    P.stage_bytes = P.n_perlin_lds * RTL_PERLIN_BYTES;
+  }
+  P.o_mats = sc->o_mats;
+  P.o_texs = sc->o_texs;
+  P.o_lights = sc->o_lights;
+  P.o_loffs = sc->o_loffs;
+  P.o_perl = sc->o_perl;
+  const size_t lds_bytes = P.stage_bytes;
   for (int k = 0; k < 3; ++k) {
     P.center[k] = cam->center[k];
     P.p00[k] = cam->pixel00_loc[k];
