@@ -9,13 +9,13 @@ BUILD    := build
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 # device path is f64; contraction off, fma written explicitly (deterministic bits)
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS := --offload-arch=$(ARCH) -Iinclude -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra
 CFLAGS_O := -std=c11 -O2 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
 HOST_SRC := $(CSRC)/host/scene.cpp $(CSRC)/host/presets.cpp $(CSRC)/host/capi.cpp
 DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp
-DEV_HDR  := $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp include/rt_mi355x.h
+DEV_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp include/rt_mi355x.h
 
 .PHONY: all device host oracle cli clean
 all: device host oracle cli

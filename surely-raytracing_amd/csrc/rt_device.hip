@@ -22,1156 +22,25 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
-#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
 
-#include "../../include/rt_mi355x.h"
+#include "rt_mi355x.h"
 #include "rt_flatten.hpp"
+#include "rt_kernel.h"
 #include "rt_layout.h"
-#include "rt_rng.h"
 
-using namespace rtd;
+using namespace rtk;
 
 namespace {
 
-// The path is computed in f64 like the reference (vec3.rs:21-25 f64 everywhere): its fixed
-// epsilons (t_min 1e-4 render.rs:267, 1e-3 light PDFs object.rs:193,493, 1e-8 quad
-// parallelism object.rs:457) assume f64 hit points; at fp32 the glass sphere and the ground
-// boxes self-intersect. MI355X runs FP64 FMA at half its FP32 rate.
-constexpr double kPi = 3.14159265358979323846;
-constexpr int kWaveTile = 8;  // 8x8 pixels per wave
-constexpr int kBlock = 256;   // 4 waves per workgroup
-// Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument). 4 caps the
-// allocation at 128 VGPRs. Kernels with a per-lane BVH walker need more than that without
-// spilling inside the walk, and spills there cost more than the occupancy they buy: 2 waves
-// (256 VGPRs) measured 294 vs 214 Msamples/s on final_scene; volume/texture kernels without a
-// BVH stay at 4 (cornell_smoke: 2221 at 4 vs 1985 at 2). tools_gpu/ab_variants.py, variants-occ.
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 4
-#endif
-#ifndef RT_MIN_WAVES_BVH
-#define RT_MIN_WAVES_BVH 2
-#endif
-template <bool VOL, bool TEX, bool BVH>
-struct MinWaves {
-  static constexpr int value = BVH ? RT_MIN_WAVES_BVH : RT_MIN_WAVES;
-};
-
-struct d3 {
-  double x, y, z;
-};
-__device__ __forceinline__ d3 mk(double x, double y, double z) { return {x, y, z}; }
-__device__ __forceinline__ d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ d3 operator-(d3 a) { return {-a.x, -a.y, -a.z}; }
-__device__ __forceinline__ d3 operator*(d3 a, d3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
-__device__ __forceinline__ d3 operator*(d3 a, double t) { return {a.x * t, a.y * t, a.z * t}; }
-__device__ __forceinline__ d3 operator*(double t, d3 a) { return {a.x * t, a.y * t, a.z * t}; }
-// Contraction is OFF for the device build (-ffp-contract=off): every fma below is explicit, so
-// an expression computes the same bits in every inlining context. The reference relies on
-// that determinism: a sphere that is both a world object and a ConstantMedium boundary
-// (main.rs:656-666) must yield the identical t from both tests, or constant_medium.rs:52-55
-// draws an extra random number.
-__device__ __forceinline__ double dot(d3 u, d3 v) {  // vec3.rs:167
-  return fma(u.x, v.x, fma(u.y, v.y, u.z * v.z));
-}
-__device__ __forceinline__ d3 vfma(double t, d3 a, d3 b) {  // t*a + b
-  return {fma(t, a.x, b.x), fma(t, a.y, b.y), fma(t, a.z, b.z)};
-}
-__device__ __forceinline__ d3 cross(d3 u, d3 v) {  // vec3.rs:171-177
-  return {fma(u.y, v.z, -(u.z * v.y)), fma(u.z, v.x, -(u.x * v.z)), fma(u.x, v.y, -(u.y * v.x))};
-}
-// Geometry-side reciprocal and reciprocal square root: the hardware v_rcp_f64 / v_rsq_f64
-// estimate plus two Newton-Raphson steps (quadratic convergence: full f64 accuracy, within an
-// ulp of the IEEE quotient, at about half the instructions of the IEEE division / sqrt
-// sequences). Used only where the operand is finite and non-zero by construction (quad
-// denominators past the 1e-8 test, |d|^2, |v|^2 of non-degenerate vectors); radiance weights
-// keep IEEE division so 0/0 stays NaN exactly as in the reference.
-__device__ __forceinline__ double rcp_nr(double b) {
-  double r = __builtin_amdgcn_rcp(b);
-  r = fma(fma(-b, r, 1.0), r, r);
-  return fma(fma(-b, r, 1.0), r, r);
-}
-__device__ __forceinline__ double div_nr(double a, double b) {
-  double r = rcp_nr(b);
-  double q = a * r;
-  return fma(fma(-b, q, a), r, q);
-}
-__device__ __forceinline__ double rsq_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double h = 0.5 * x;
-  y = y * fma(-h * y, y, 1.5);
-  return y * fma(-h * y, y, 1.5);
-}
-__device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
-  return v * rsq_nr(dot(v, v));
-}
-__device__ __forceinline__ d3 reflect(d3 v, d3 n) {  // vec3.rs:219-221
-  return vfma(-2.0 * dot(v, n), n, v);
-}
-__device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-229
-  double c = fmin(dot(-uv, n), 1.0);
-  d3 perp = e * vfma(c, n, uv);
-  return vfma(-sqrt(fabs(1.0 - dot(perp, perp))), n, perp);
-}
-
-// sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (vec3.rs:244, object.rs:127: phi = 2*pi*r1).
-// Exact reduction to a quarter-turn fraction r in [-1/2, 1/2], then Taylor series of
-// theta = r*pi/2 (|theta| <= pi/4) to theta^19 / theta^18: < 1 ulp, and none of the large-
-// argument machinery of the general sincos (which cost ~40 VGPRs here).
-__device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
-  double t = 4.0 * u;
-  double k = floor(t + 0.5);
-  double th = (t - k) * (0.5 * kPi);
-  double x2 = th * th;
-  double s = 1.0 / 121645100408832000.0;  // 1/19!
-  s = s * -x2 + 1.0 / 355687428096000.0;
-  s = s * -x2 + 1.0 / 1307674368000.0;
-  s = s * -x2 + 1.0 / 6227020800.0;
-  s = s * -x2 + 1.0 / 39916800.0;
-  s = s * -x2 + 1.0 / 362880.0;
-  s = s * -x2 + 1.0 / 5040.0;
-  s = s * -x2 + 1.0 / 120.0;
-  s = s * -x2 + 1.0 / 6.0;
-  s = (s * -x2 + 1.0) * th;
-  double c = 1.0 / 6402373705728000.0;  // 1/18!
-  c = c * -x2 + 1.0 / 20922789888000.0;
-  c = c * -x2 + 1.0 / 87178291200.0;
-  c = c * -x2 + 1.0 / 479001600.0;
-  c = c * -x2 + 1.0 / 3628800.0;
-  c = c * -x2 + 1.0 / 40320.0;
-  c = c * -x2 + 1.0 / 720.0;
-  c = c * -x2 + 1.0 / 24.0;
-  c = c * -x2 + 0.5;
-  c = c * -x2 + 1.0;
-  int q = ((int)k) & 3;
-  *so = q == 0 ? s : (q == 1 ? c : (q == 2 ? -s : -c));
-  *co = q == 0 ? c : (q == 1 ? -s : (q == 2 ? -c : s));
-}
-
-// Perlin tables staged per workgroup (dynamic LDS of the TEX kernels: n_perlin_lds tables)
-constexpr uint32_t kPerlinLds = 4;
-// Scenes whose node/material/texture/light tables (+ Perlin tables) fit this many bytes are
-// staged in LDS whole: 4 workgroups per CU x 24 KiB stay well inside the CU's 160 KiB.
-constexpr size_t kStageScene = 24u << 10;
-extern __shared__ __attribute__((aligned(16))) uint8_t rt_lds[];
-
-// Table pointers for per-lane (divergent) reads: the workgroup's LDS copy of a small scene, or
-// the global tables. Generic pointers: the same code reads either.
-struct Tabs {
-  const uint32_t *nodes, *mats, *texs, *lights, *loffs;
-  const uint8_t* perlin;  // LDS: the staged Perlin tables
-};
-
-struct TraceParams {
-  const uint32_t* __restrict__ nodes;
-  const uint32_t* __restrict__ mats;
-  const uint32_t* __restrict__ texs;
-  const uint8_t* __restrict__ perlin;
-  const uint32_t* __restrict__ lights;
-  const uint32_t* __restrict__ light_offs;
-  const uint8_t* __restrict__ texels;
-  float* __restrict__ samp;  // per-sample radiance, [wave][pool item] x RGB (item = s_i*nv + pv)
-  unsigned long long* __restrict__ ops;
-  unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  int n_pools;                       // pools of this launch: tiles x n_sj
-  uint32_t root, n_lights, lights_is_list, flags;
-  uint32_t n_perlin_lds;  // Perlin tables readable from LDS (TEX kernels)
-  // LDS staging (rt_trace prologue): stage_bytes of the scene allocation starting at stage_src.
-  // stage_scene = 1: the whole small-table prefix [nodes .. Perlin] is copied, and per-lane
-  // (divergent) reads of nodes / materials / textures / lights use the copy; 0: only the first
-  // n_perlin_lds Perlin tables are copied. Offsets are bytes from the start of the allocation.
-  const uint8_t* stage_src;
-  uint32_t stage_bytes, stage_scene;
-  uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
-  double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
-  double rs;
-  int defocus;
-  int W, n_rows, row_begin, row_step, sqrt_spp, sj0, n_sj, max_depth;
-  uint32_t seed_lo, seed_hi;
-  int tiles_x;
-};
-
-// The kernel's only argument sits at offset 0 of the kernarg segment. Camera constants are read
-// through this pointer at their point of use; the empty asm makes the pointer opaque so the loads
-// are not hoisted out of the path loop, where ~40 loop-invariant SGPRs would spill to VGPR lanes.
-typedef const __attribute__((address_space(4))) TraceParams* kparams_t;
-__device__ __forceinline__ kparams_t kparams() {
-  kparams_t p = (kparams_t)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
-}
-__device__ __forceinline__ d3 karr3(const __attribute__((address_space(4))) double* a) {
-  return {a[0], a[1], a[2]};
-}
-
-// ---------------------------------------------------------------- loads
-// Two pointer kinds reach the same node records:
-//  gptr: per-lane (divergent) node index -> vector loads (global_load_dwordx4 through L1/L2)
-//  kptr: wave-uniform node index (no BVH: every lane walks the same node sequence) -> the
-//        constant address space lets hipcc use scalar loads (s_load_dwordx*, K$), so node
-//        data lands in SGPRs and costs neither VGPRs nor vector-memory latency.
-typedef const uint32_t* gptr;
-typedef const __attribute__((address_space(4))) uint32_t* kptr;
-typedef const __attribute__((address_space(4))) double* kdptr;
-
-__device__ __forceinline__ d3 ld3(gptr X, int k) {  // f64 triple at payload double index k
-  const double* d = reinterpret_cast<const double*>(X + 4) + k;
-  if ((k & 1) == 0) {
-    double2 a = *reinterpret_cast<const double2*>(d);
-    return mk(a.x, a.y, d[2]);
-  }
-  double2 b = *reinterpret_cast<const double2*>(d + 1);
-  return mk(d[0], b.x, b.y);
-}
-__device__ __forceinline__ d3 ld3(kptr X, int k) {
-  kdptr d = reinterpret_cast<kdptr>(X + 4) + k;
-  return mk(d[0], d[1], d[2]);
-}
-__device__ __forceinline__ double ldd(gptr X, int k) {
-  return reinterpret_cast<const double*>(X + 4)[k];
-}
-__device__ __forceinline__ double ldd(kptr X, int k) { return reinterpret_cast<kdptr>(X + 4)[k]; }
-__device__ __forceinline__ uint4 ld4u(gptr p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ uint4 ld4u(kptr p) { return make_uint4(p[0], p[1], p[2], p[3]); }
-// first 64 bytes of a node record: four independent 16-byte loads, one memory round trip
-template <class Ptr>
-__device__ __forceinline__ void ld64(Ptr p, uint4& a, uint4& b, uint4& c, uint4& e) {
-  a = ld4u(p);
-  b = ld4u(p + 4);
-  c = ld4u(p + 8);
-  e = ld4u(p + 12);
-}
-__device__ __forceinline__ d3 arr3(const double* a) { return mk(a[0], a[1], a[2]); }
-
-// ---------------------------------------------------------------- op counters (COUNT build)
-template <bool COUNT>
-struct Ctr {
-  __device__ __forceinline__ void inc(int) {}
-  __device__ __forceinline__ void inc_if(int, bool) {}
-  __device__ __forceinline__ void flush(unsigned int*) {}
-};
-template <>
-struct Ctr<true> {
-  uint32_t c[RT_OP_COUNT];
-  __device__ Ctr() {
-#pragma unroll
-    for (int k = 0; k < RT_OP_COUNT; ++k) c[k] = 0;
-  }
-  __device__ __forceinline__ void inc(int k) { c[k]++; }
-  __device__ __forceinline__ void inc_if(int k, bool b) { c[k] += b ? 1u : 0u; }
-  __device__ void flush(unsigned int* sh) {
-#pragma unroll
-    for (int k = 0; k < RT_OP_COUNT; ++k)
-      if (c[k]) atomicAdd(&sh[k], c[k]);
-  }
-};
-
-// ---------------------------------------------------------------- primitives
-// Quad::hit object.rs:453-490; inclusive interval (Interval::contains interval.rs:21-23).
-// Branch-free: every lane evaluates the whole test and the outcome is a predicate, so a wave
-// walks the quad in one straight-line block (no exec-mask churn, loads of the next node can be
-// hoisted). Rejections follow the reference's order and NaN behaviour exactly:
-// |n.d| < 1e-8 -> miss; !(tmin <= t <= tmax) -> miss; a < 0 || 1 < a || b < 0 || 1 < b -> miss.
-template <bool COUNT, class Ptr>
-__device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double tmax,
-                                          double& t_out, Ctr<COUNT>& C) {
-  C.inc(RT_OP_QUAD_TESTS);
-  d3 n = ld3(q, 0);
-  double denom = dot(n, d);
-  double t = div_nr(ldd(q, 3) - dot(n, o), denom);
-  d3 pq = vfma(t, d, o) - ld3(q, 4);
-  double a = dot(pq, ld3(q, 8));
-  double b = dot(pq, ld3(q, 12));
-  bool plane = !(fabs(denom) < 1e-8);
-  bool range = plane && (tmin <= t && t <= tmax);
-  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
-  C.inc_if(RT_OP_QUAD_PLANE, plane);
-  C.inc_if(RT_OP_QUAD_INTERVAL, range);
-  C.inc_if(RT_OP_QUAD_HITS, hit);
-  if (hit) t_out = t;
-  return hit;
-}
-
-// The same test for an axis-aligned quad (rt_layout.h RTL_QUAD_AXIS): bit-identical results,
-// with r = rcp_nr(d) computed once per batch instead of once per quad.
-template <int K>
-__device__ __forceinline__ double comp(d3 v) {
-  return K == 0 ? v.x : (K == 1 ? v.y : v.z);
-}
-__device__ __forceinline__ double hilo(uint32_t lo, uint32_t hi) {
-  return __hiloint2double((int)hi, (int)lo);
-}
-struct AQuad {  // the first 64 bytes of a world QUAD record
-  uint32_t h0;
-  double qk, qlo, clo, qhi, chi;
-};
-template <class Ptr>
-__device__ __forceinline__ AQuad load_aquad(Ptr Q) {
-  const uint4 a = ld4u(Q), b = ld4u(Q + 4), c = ld4u(Q + 8), e = ld4u(Q + 12);
-  return {a.x, hilo(b.x, b.y), hilo(b.z, b.w), hilo(c.x, c.y), hilo(c.z, c.w), hilo(e.x, e.y)};
-}
-template <bool COUNT, int K>
-__device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, double tmin,
-                                           double tmax, double& t_out, Ctr<COUNT>& C) {
-  constexpr int LO = K == 0 ? 1 : 0, HI = K == 2 ? 1 : 2;
-  C.inc(RT_OP_QUAD_TESTS);
-  const double dk = comp<K>(d), rk = comp<K>(r);
-  const double num = q.qk - comp<K>(o);
-  const double t0 = num * rk;
-  const double t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
-  const double a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
-  const double b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
-  bool plane = !(fabs(dk) < 1e-8);
-  bool range = plane && (tmin <= t && t <= tmax);
-  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
-  C.inc_if(RT_OP_QUAD_PLANE, plane);
-  C.inc_if(RT_OP_QUAD_INTERVAL, range);
-  C.inc_if(RT_OP_QUAD_HITS, hit);
-  if (hit) t_out = t;
-  return hit;
-}
-// A world QUAD record (batch member or single): branch on its axis code (wave-uniform in UNI
-// traversal); r = rcp_nr(d) of the current frame.
-template <bool COUNT, class Ptr>
-__device__ __forceinline__ bool world_quad_test(Ptr Q, d3 o, d3 d, d3 r, double tmin, double tmax,
-                                                double& t_out, Ctr<COUNT>& C) {
-  const AQuad q = load_aquad(Q);
-  switch (RTL_QUAD_AXIS(q.h0)) {
-    case 1u: return aquad_test<COUNT, 0>(q, o, d, r, tmin, tmax, t_out, C);
-    case 2u: return aquad_test<COUNT, 1>(q, o, d, r, tmin, tmax, t_out, C);
-    case 3u: return aquad_test<COUNT, 2>(q, o, d, r, tmin, tmax, t_out, C);
-    default: return quad_test<COUNT>(Q + RTL_QUAD_GEN, o, d, tmin, tmax, t_out, C);
-  }
-}
-
-// world_quad_test on an axis-aligned form already in registers (Q = the record, for the
-// general payload of a non-axis-aligned quad).
-template <bool COUNT, class Ptr>
-__device__ __forceinline__ bool aquad_dispatch(const AQuad& q, Ptr Q, d3 o, d3 d, d3 r,
-                                               double tmin, double tmax, double& t_out,
-                                               Ctr<COUNT>& C) {
-  switch (RTL_QUAD_AXIS(q.h0)) {
-    case 1u: return aquad_test<COUNT, 0>(q, o, d, r, tmin, tmax, t_out, C);
-    case 2u: return aquad_test<COUNT, 1>(q, o, d, r, tmin, tmax, t_out, C);
-    case 3u: return aquad_test<COUNT, 2>(q, o, d, r, tmin, tmax, t_out, C);
-    default: return quad_test<COUNT>(Q + RTL_QUAD_GEN, o, d, tmin, tmax, t_out, C);
-  }
-}
-
-// Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
-template <bool COUNT, class Ptr>
-__device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double tmin,
-                                            double tmax, double& t_out, Ctr<COUNT>& C) {
-  C.inc(RT_OP_SPHERE_TESTS);
-  d3 center = ld3(s, 0);
-  double r = ldd(s, 3);
-  if (s[3]) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
-  d3 oc = o - center;
-  double a = dot(d, d);
-  double half_b = dot(oc, d);
-  double c = dot(oc, oc) - r * r;
-  double disc = fma(half_b, half_b, -(a * c));
-  if (disc < 0.0) return false;
-  C.inc(RT_OP_SPHERE_ROOTS);
-  double sqrtd = sqrt(disc);
-  double ra = rcp_nr(a);
-  double root = (-half_b - sqrtd) * ra;
-  if (!(tmin < root && root < tmax)) {
-    root = (sqrtd - half_b) * ra;
-    if (!(tmin < root && root < tmax)) return false;
-  }
-  C.inc(RT_OP_SPHERE_HITS);
-  t_out = root;
-  return true;
-}
-
-// Aabb::hit object.rs:340-370 on bounds already in registers (the LANE walker's 64-byte node
-// fetch), with inv_d = 1/d computed once per ray frame.
-__device__ __forceinline__ bool aabb_hit(const double (&mn)[3], const double (&mx)[3], d3 o,
-                                         d3 inv, double tmin, double tmax) {
-  const double oo[3] = {o.x, o.y, o.z}, id[3] = {inv.x, inv.y, inv.z};
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    double t0 = (mn[a] - oo[a]) * id[a];
-    double t1 = (mx[a] - oo[a]) * id[a];
-    if (id[a] < 0.0) {
-      double tt = t0;
-      t0 = t1;
-      t1 = tt;
-    }
-    if (t0 > tmin) tmin = t0;
-    if (t1 < tmax) tmax = t1;
-    if (tmax <= tmin) return false;
-  }
-  return true;
-}
-
-// Translate/RotateY ray into object space (transform.rs:59, 86-107).
-template <class Ptr>
-__device__ __forceinline__ void xform_in(Ptr X, d3& o, d3& d) {
-  if ((X[0] & 0xffu) == RTL_TRANSLATE) {
-    o = o - ld3(X, 2);
-  } else {
-    double s = ldd(X, 2), c = ldd(X, 3);
-    o = mk(fma(c, o.x, -(s * o.z)), o.y, fma(s, o.x, c * o.z));
-    d = mk(fma(c, d.x, -(s * d.z)), d.y, fma(s, d.x, c * d.z));
-  }
-}
-// Hit record back to the parent space (transform.rs:65, 114-130).
-__device__ __forceinline__ void xform_out(gptr X, d3& p, d3& n) {
-  if ((X[0] & 0xffu) == RTL_TRANSLATE) {
-    p = p + ld3(X, 2);
-  } else {
-    double s = ldd(X, 2), c = ldd(X, 3);
-    p = mk(fma(c, p.x, s * p.z), p.y, fma(-s, p.x, c * p.z));
-    n = mk(fma(c, n.x, s * n.z), n.y, fma(-s, n.x, c * n.z));
-  }
-}
-// Local ray of `frame` = the world ray pushed through its transform chain, root first.
-template <class Ptr>
-__device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o, d3& d) {
-  o = wo;
-  d = wd;
-  if (frame < 0) return;
-  uint4 h = ld4u(N + frame);
-  uint4 ch = ld4u(N + frame + 4);
-  const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-  for (int k = 0; k < RTL_MAX_CHAIN; ++k)
-    if ((uint32_t)k < h.z) xform_in(N + c4[k], o, d);
-}
-
-// ---------------------------------------------------------------- traversal
-// Threaded walk of the flattened scene (rt_layout.h). MAIN: the world (records the hit node and
-// its frame, handles ConstantMedium when VOL). !MAIN: a volume boundary (closest t only).
-//
-// Two walkers share this body:
-//  UNI  (wave-uniform): outside BVH subtrees the node sequence does not depend on the ray (lists,
-//       transforms, volumes and primitives are visited in a fixed order), so the node index is
-//       readfirstlane'd and node records arrive by scalar loads (K$, SGPRs, no VGPRs). Used for
-//       every scene's top level.
-//  LANE (per-lane): inside a BVH subtree each lane follows its own skip links. Each node's first
-//       64 bytes (header + bbox, or header + axis-aligned quad form) are fetched by four
-//       independent 16-byte vector loads, so one memory round trip serves a BVH node. The UNI
-//       walker hands a BVH subtree [root, skip) to the LANE walker with the current closest-hit
-//       state and resumes at its skip once every lane has finished it (BVH = the scene has one).
-template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH>
-__device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
-                         double tm, d3 o, d3 d, int frame, double tmin, double tmax,
-                         double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
-                         Ctr<COUNT>& C) {
-  typedef typename std::conditional<UNI, kptr, gptr>::type Ptr;
-  const Ptr N = (Ptr)P.nodes;
-  double closest = tmax;
-  bool hit = false;
-  d3 inv = mk(0., 0., 0.);
-  bool inv_ok = false;
-  for (;;) {
-    uint4 h, q1, q2, q3;
-    if (UNI) {
-      node = __builtin_amdgcn_readfirstlane(node);
-      frame = __builtin_amdgcn_readfirstlane(frame);
-      h = ld4u(N + node);
-    } else {
-      if (node == stop) break;
-      // speculative 64-byte fetch (the node array is padded past its END)
-      ld64(N + node, h, q1, q2, q3);
-      // while-while: a lane steps through BVH nodes until it reaches a leaf (or the subtree's
-      // end); lanes that got there first wait at the loop exit, so the leaf bodies below run
-      // with every lane that has a leaf instead of interleaving with the AABB steps.
-      while ((h.x & 0xffu) == RTL_BVH) {
-        C.inc(RT_OP_AABB_TESTS);
-        if (!inv_ok) {
-          inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-          inv_ok = true;
-        }
-        const double mn[3] = {hilo(q1.x, q1.y), hilo(q2.x, q2.y), hilo(q3.x, q3.y)};
-        const double mx[3] = {hilo(q1.z, q1.w), hilo(q2.z, q2.w), hilo(q3.z, q3.w)};
-        node = aabb_hit(mn, mx, o, inv, tmin, closest) ? node + RTL_BVH_WORDS : h.y;
-        if (node == stop) break;
-        ld64(N + node, h, q1, q2, q3);
-      }
-      if (node == stop) break;
-    }
-    const Ptr X = N + node;
-    uint32_t type = h.x & 0xffu;
-    if (type == RTL_QUAD) {
-      double t;
-      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
-      bool hq;
-      if (UNI) {
-        hq = world_quad_test<COUNT>(X, o, d, r, tmin, closest, t, C);
-      } else {
-        const AQuad q = {h.x, hilo(q1.x, q1.y), hilo(q1.z, q1.w), hilo(q2.x, q2.y),
-                         hilo(q2.z, q2.w), hilo(q3.x, q3.y)};
-        hq = aquad_dispatch<COUNT>(q, X, o, d, r, tmin, closest, t, C);
-      }
-      if (hq) {
-        closest = t;
-        hit = true;
-        if (MAIN) {
-          hit_node = node;
-          hit_frame = frame;
-        }
-      }
-      node += RTL_QUAD_WORDS;
-    } else if (type == RTL_QUADS) {
-      // batch of sibling quads: the same sequential closest-hit updates as the list
-      const uint32_t cnt = h.x >> 8;
-      Ptr Q = X + 4;
-      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
-      uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
-      if (!UNI) ld64(Q, a0, a1, a2, a3);
-      for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
-        double t;
-        bool hq;
-        if (UNI) {
-          hq = world_quad_test<COUNT>(Q, o, d, r, tmin, closest, t, C);
-        } else {
-          const AQuad q = {a0.x, hilo(a1.x, a1.y), hilo(a1.z, a1.w), hilo(a2.x, a2.y),
-                           hilo(a2.z, a2.w), hilo(a3.x, a3.y)};
-          ld64(Q + RTL_QUAD_WORDS, a0, a1, a2, a3);  // past the batch: the next node (padded)
-          hq = aquad_dispatch<COUNT>(q, Q, o, d, r, tmin, closest, t, C);
-        }
-        if (hq) {
-          closest = t;
-          hit = true;
-          if (MAIN) {
-            hit_node = (uint32_t)(node + 4 + k * RTL_QUAD_WORDS);
-            hit_frame = frame;
-          }
-        }
-      }
-      node = h.y;
-    } else if (type == RTL_SPHERE) {
-      double t;
-      if (sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C)) {
-        closest = t;
-        hit = true;
-        if (MAIN) {
-          hit_node = node;
-          hit_frame = frame;
-        }
-      }
-      node += RTL_SPHERE_WORDS;
-    } else if (type == RTL_BVH) {
-      if (UNI) {
-        if (BVH) {  // the subtree [node, skip) per lane, continuing this walk's closest hit
-          double t;
-          uint32_t hn;
-          int hf;
-          if (traverse<MAIN, COUNT, VOL, false, BVH>(P, node, h.y, wo, wd, tm, o, d, frame, tmin,
-                                                     closest, t, hn, hf, g, C)) {
-            closest = t;
-            hit = true;
-            if (MAIN) {
-              hit_node = hn;
-              hit_frame = hf;
-            }
-          }
-        }
-        node = h.y;
-      }  // LANE: BVH nodes never get here (the while-while step above consumes them)
-    } else if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y) {
-      C.inc(type == RTL_TRANSLATE ? RT_OP_TRANSLATE : RT_OP_ROTATE_Y);
-      xform_in(X, o, d);
-      if (type == RTL_ROTATE_Y) inv_ok = false;
-      frame = (int)node;
-      node += RTL_XFORM_WORDS;
-    } else if (type == RTL_EXIT) {
-      frame = (int)h.z;
-      frame_ray(N, frame, wo, wd, o, d);
-      inv_ok = false;
-      node += RTL_EXIT_WORDS;
-    } else if (MAIN && VOL && type == RTL_VOLUME) {
-      // ConstantMedium::hit constant_medium.rs:41-95
-      C.inc(RT_OP_VOLUME_TESTS);
-      // rec1 = boundary.hit(r, (-inf, inf)), rec2 = boundary.hit(r, [rec1.t + 1e-4, inf)):
-      // one rolled loop, so the boundary walker is instantiated once
-      double t1 = 0.0, t2 = 0.0;
-      bool both = true;
-#pragma unroll 1
-      for (int pass = 0; pass < 2 && both; ++pass) {
-        double tb;
-        uint32_t dn;
-        int df;
-        both = traverse<false, COUNT, false, UNI, BVH>(P, node + RTL_VOLUME_WORDS, ~0u, wo, wd, tm,
-                                                       o, d, frame,
-                                                       pass ? t1 + 0.0001 : -INFINITY, INFINITY,
-                                                       tb, dn, df, g, C);
-        if (pass) t2 = tb; else t1 = tb;
-      }
-      if (both) {
-        if (t1 < tmin) t1 = tmin;
-        if (t2 > closest) t2 = closest;
-        if (t1 < t2) {
-          if (t1 < 0.0) t1 = 0.0;
-          double ray_length = sqrt(dot(d, d));
-          double dist_inside = (t2 - t1) * ray_length;
-          C.inc(RT_OP_VOLUME_DRAWS);
-          double hit_distance = ldd(X, 0) * log(rnd(g));
-          if (!(hit_distance > dist_inside)) {
-            closest = t1 + hit_distance / ray_length;
-            hit = true;
-            hit_node = node;
-            hit_frame = frame;
-          }
-        }
-      }
-      node = h.y;
-    } else if (type == RTL_END) {
-      break;
-    } else {
-      node = h.y;
-    }
-  }
-  t_out = closest;
-  return hit;
-}
-
-// ---------------------------------------------------------------- textures
-__device__ __forceinline__ int32_t f2i_sat(double f) {  // Rust `as i32`
-  if (f != f) return 0;
-  if (f >= 2147483648.0) return INT32_MAX;
-  if (f <= -2147483648.0) return INT32_MIN;
-  return (int32_t)f;
-}
-__device__ __forceinline__ uint32_t f2u_sat(double f) {  // Rust `as u32`
-  if (f != f || f <= 0.0) return 0u;
-  if (f >= 4294967296.0) return UINT32_MAX;
-  return (uint32_t)f;
-}
-
-// Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96. T = one table
-// (RTL_PERLIN_BYTES: ranvec as 256 double4, then perm_x/y/z), normally the workgroup's LDS copy
-// (rt_trace stages the scene's first kPerlinLds tables at launch). The octave loop stays rolled
-// and each octave reads the six permutation entries once, so the eight corner gathers are the
-// only wide live values.
-__device__ __forceinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) {
-  const double* rv = reinterpret_cast<const double*>(T);
-  const uint8_t* px = T + 8192;
-  const uint8_t* py = px + 256;
-  const uint8_t* pz = py + 256;
-  double accum = 0.0, weight = 1.0;
-#pragma unroll 1
-  for (int oct = 0; oct < 7; ++oct) {
-    double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
-    double u = p.x - fx, v = p.y - fy, w = p.z - fz;
-    const uint32_t i = (uint32_t)f2i_sat(fx), j = (uint32_t)f2i_sat(fy), k = (uint32_t)f2i_sat(fz);
-    const uint32_t X[2] = {px[i & 255u], px[(i + 1u) & 255u]};
-    const uint32_t Y[2] = {py[j & 255u], py[(j + 1u) & 255u]};
-    const uint32_t Z[2] = {pz[k & 255u], pz[(k + 1u) & 255u]};
-    double uu = u * u * (3.0 - 2.0 * u);
-    double vv = v * v * (3.0 - 2.0 * v);
-    double ww = w * w * (3.0 - 2.0 * w);
-    double acc = 0.0;
-#pragma unroll
-    for (int di = 0; di < 2; ++di)
-#pragma unroll
-      for (int dj = 0; dj < 2; ++dj)
-#pragma unroll
-        for (int dk = 0; dk < 2; ++dk) {
-          const uint32_t idx = X[di] ^ Y[dj] ^ Z[dk];
-          double2 cxy = *reinterpret_cast<const double2*>(rv + 4 * idx);
-          d3 c = mk(cxy.x, cxy.y, rv[4 * idx + 2]);
-          double wi = di ? uu : 1.0 - uu;
-          double wj = dj ? vv : 1.0 - vv;
-          double wk = dk ? ww : 1.0 - ww;
-          d3 wv = mk(u - (double)di, v - (double)dj, w - (double)dk);
-          acc = fma(wi * wj * wk, dot(c, wv), acc);
-        }
-    accum = fma(weight, acc, accum);
-    weight *= 0.5;
-    p = p * 2.0;
-  }
-  return fabs(accum);
-}
-// Tables past the LDS-staged ones (scenes with more than kPerlinLds noise textures): global.
-__device__ __noinline__ double perlin_turb_global(const uint8_t* __restrict__ T, d3 p) {
-  return perlin_turb(T, p);
-}
-
-template <bool COUNT, bool TEX>
-__device__ d3 tex_value(const TraceParams& P, const Tabs& T, uint32_t id, double u, double v,
-                        d3 p, Ctr<COUNT>& C) {
-  if (!TEX) return ld3(T.texs + (size_t)id * RTL_TEX_WORDS, 0);
-  for (int guard = 0; guard < 65; ++guard) {
-    const uint32_t* t = T.texs + (size_t)id * RTL_TEX_WORDS;
-    uint4 h = ld4u(t);
-    if (h.x == RT_TEX_SOLID) return ld3(t, 0);
-    if (h.x == RT_TEX_CHECKER) {  // texture.rs:71-81
-      double is = ldd(t, 0);
-      int32_t x = f2i_sat(floor(is * p.x));
-      int32_t y = f2i_sat(floor(is * p.y));
-      int32_t z = f2i_sat(floor(is * p.z));
-      uint32_t sum = (uint32_t)x + (uint32_t)y + (uint32_t)z;
-      id = (sum & 1u) == 0u ? h.y : h.z;
-      continue;
-    }
-    if (h.x == RT_TEX_IMAGE) {  // texture.rs:95-107, rt_image.rs:37-46
-      int W = (int)h.y, H = (int)h.z;
-      if (H <= 0 || W <= 0) return mk(0., 1., 1.);
-      double cu = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);
-      double cv = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);
-      uint32_t i = f2u_sat(cu * (double)W);
-      uint32_t j = f2u_sat(cv * (double)H);
-      uint32_t x = i < (uint32_t)(W - 1) ? i : (uint32_t)(W - 1);
-      uint32_t y = (uint32_t)H - j - 1u;
-      if (y > (uint32_t)(H - 1)) y = (uint32_t)(H - 1);
-      const uint8_t* px = P.texels + h.w + ((size_t)y * W + x) * 3;
-      const double cs = 1.0 / 255.0;
-      return mk((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
-    }
-    if (h.x == RT_TEX_NOISE) {  // texture.rs:127-130
-      C.inc(RT_OP_NOISE_EVALS);
-      d3 s = p * ldd(t, 0);
-      double turb = h.y < P.n_perlin_lds
-                        ? perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
-                        : perlin_turb_global(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
-      double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
-      return mk(k, k, k);
-    }
-    break;
-  }
-  return mk(0., 0., 0.);
-}
-
-// get_sphere_uv object.rs:114-120 (out of line: only image-textured spheres need it)
-__device__ __noinline__ void sphere_uv(d3 p, double& u, double& v) {
-  double theta = acos(-p.y);
-  double phi = atan2(-p.z, p.x) + kPi;
-  u = phi * (1.0 / kPi) * 0.5;
-  v = theta * (1.0 / kPi);
-}
-
-// ---------------------------------------------------------------- sampling
-struct Onb {
-  d3 u, v, w;
-};
-__device__ __forceinline__ d3 onb_local(const Onb& b, d3 a) {  // onb.rs:24-26
-  return vfma(a.x, b.u, vfma(a.y, b.v, b.w * a.z));
-}
-__device__ __forceinline__ d3 random_cosine_direction(Rng& g) {  // vec3.rs:240-250
-  double r1 = rnd(g);
-  double r2 = rnd(g);
-  double s, c;
-  sincos2pi(r1, &s, &c);
-  double sq = sqrt(r2);
-  return mk(c * sq, s * sq, sqrt(1.0 - r2));
-}
-__device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 231-238
-  for (;;) {
-    double x = rnd_pm1(g);
-    double y = rnd_pm1(g);
-    double z = rnd_pm1(g);
-    d3 p = mk(x, y, z);
-    if (dot(p, p) < 1.0) return unit_vector(p);
-  }
-}
-
-// Light-list PDF value (HittablePDF::value pdf.rs:91-93 -> HittableList::pdf_value
-// hittable.rs:115-124 -> Quad/Sphere::pdf_value object.rs:492-501, 190-202).
-template <bool COUNT>
-__device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>& C) {
-  double sum = 0.0;
-  for (uint32_t i = 0; i < P.n_lights; ++i) {
-    const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
-    uint32_t type = L[0] & 0xffu;
-    double pv = 0.0;
-    if (type == RTL_QUAD) {
-      C.inc(RT_OP_LIGHT_PDF_QUAD);
-      double t;
-      if (quad_test<COUNT>(L, origin, dir, 0.001, INFINITY, t, C)) {
-        double len2 = dot(dir, dir);
-        double dist2 = (t * t) * len2;
-        double cosine = fabs(dot(dir, ld3(L, 0)) / sqrt(len2));
-        pv = dist2 / (cosine * ldd(L, 7));
-      }
-    } else if (type == RTL_SPHERE) {
-      C.inc(RT_OP_LIGHT_PDF_SPHERE);
-      double t;
-      if (sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, INFINITY, t, C)) {
-        d3 c = ld3(L, 0);
-        double r = ldd(L, 3);
-        d3 cmo = c - origin;
-        double cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
-        double solid = 2.0 * kPi * (1.0 - cos_max);
-        pv = 1.0 / solid;
-      }
-    }
-    sum = i == 0 ? pv : sum + pv;
-  }
-  return P.lights_is_list ? sum * (1.0 / (double)P.n_lights) : sum;
-}
-
-__device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t slot, d3 L) {
-  float* o = samp + slot * 3;
-  o[0] = (float)L.x;
-  o[1] = (float)L.y;
-  o[2] = (float)L.z;
-}
-
-// ---------------------------------------------------------------- the path kernel
-// VOL: scene has ConstantMedium nodes; TEX: some material reads a non-solid texture.
+// Ahead-of-time kernels: the interpreter traversal, one per feature combination.
 template <bool COUNT, bool VOL, bool TEX, bool BVH>
 __global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(TraceParams P) {
-  __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
-  if (COUNT) {
-    for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
-    __syncthreads();
-  }
-  if (P.stage_bytes) {  // copy the small tables (or just the Perlin tables) into LDS
-    const uint4* src = reinterpret_cast<const uint4*>(P.stage_src);
-    uint4* dst = reinterpret_cast<uint4*>(rt_lds);
-    const uint32_t n16 = P.stage_bytes / 16;
-    for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
-    __syncthreads();
-  }
-  Tabs T;
-  {
-    const uint8_t* b = P.stage_scene ? (const uint8_t*)rt_lds : (const uint8_t*)P.nodes;
-    T.nodes = reinterpret_cast<const uint32_t*>(b);
-    T.mats = reinterpret_cast<const uint32_t*>(b + P.o_mats);
-    T.texs = reinterpret_cast<const uint32_t*>(b + P.o_texs);
-    T.lights = reinterpret_cast<const uint32_t*>(b + P.o_lights);
-    T.loffs = reinterpret_cast<const uint32_t*>(b + P.o_loffs);
-    T.perlin = rt_lds + (P.stage_scene ? P.o_perl : 0u);
-  }
-  Ctr<COUNT> C;
-#ifdef RT_PROF  // profiling build: wave cycles per loop section into P.ops[0..7] (not shipped)
-  unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long prof_last = __builtin_readcyclecounter();
-  int prof_sec = 0;
-  unsigned long long prof_lanes = 0, prof_iters = 0;  // lanes entering traversal, wave-iterations
-#define PROF(k)                                                  \
-  do {                                                           \
-    const unsigned long long now_ = __builtin_readcyclecounter(); \
-    prof_acc[prof_sec] += now_ - prof_last;                      \
-    prof_last = now_;                                            \
-    prof_sec = (k);                                              \
-  } while (0)
-#else
-#define PROF(k) \
-  do {          \
-  } while (0)
-#endif
-  // Persistent waves: a wave takes pools (one 8x8 tile x one stratum row s_j: nv * sqrt_spp
-  // paths) from a global queue and its lanes claim paths across pool boundaries, so lanes only
-  // idle at the very end of the launch. Wave-uniform pool state:
-  const int lane = threadIdx.x & 63;
-  int pool_id = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_j = 0;
-  bool more = true;  // the queue may still hold pools
-  const bool have_lights = P.n_lights > 0;
-  const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
-
-  d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
-  double tm = 0.;
-  int depth = 0;
-  bool alive = false;
-  size_t slot = 0;  // per-sample output slot of the path in flight
-  int next = 0;     // pool items claimed so far (wave-uniform)
-  Rng g = {0u, 0u, 0u, 0u};
-
-  for (;;) {
-    PROF(0);
-    // ---- pool scheduling: every idle lane claims the next unclaimed item (all 64 lanes are
-    // active here: lanes only ever leave the loop together)
-    const bool idle = !alive;
-    const unsigned long long want = __ballot(idle);
-    if (want != 0ull && next >= pool && more) {  // current pool drained: take the next one
-      uint32_t id = 0u;
-      if (lane == 0) id = atomicAdd(P.queue, 1u);
-      id = __builtin_amdgcn_readfirstlane(id);
-      if ((int)id < P.n_pools) {
-        pool_id = (int)id;
-        const int tile = pool_id / P.n_sj;
-        tx = tile % P.tiles_x;
-        ty = tile / P.tiles_x;
-        tile_w = min(kWaveTile, P.W - tx * kWaveTile);
-        nv = tile_w * min(kWaveTile, P.n_rows - ty * kWaveTile);
-        pool = nv * P.sqrt_spp;
-        s_j = P.sj0 + pool_id % P.n_sj;
-      } else {
-        more = false;
-        pool = 0;
-      }
-      next = 0;
-    }
-    if (idle) {
-      const int rank = (int)__builtin_amdgcn_mbcnt_hi(
-          (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-      const int k = next + rank;
-      if (k < pool) {
-        int pv, s_i, px_, py_;
-        if (nv == kWaveTile * kWaveTile) {  // full tile (wave-uniform): shifts
-          pv = k & (kWaveTile * kWaveTile - 1);
-          s_i = k >> 6;
-          px_ = pv & (kWaveTile - 1);
-          py_ = pv >> 3;
-        } else {
-          pv = k % nv;
-          s_i = k / nv;
-          px_ = pv % tile_w;
-          py_ = pv / tile_w;
-        }
-        const kparams_t Q = kparams();
-        const int x = tx * kWaveTile + px_;
-        const int kr = ty * kWaveTile + py_;
-        const int y = Q->row_begin + kr * Q->row_step;
-        slot = (size_t)pool_id * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
-        // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
-        g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
-                     (uint32_t)(s_j * Q->sqrt_spp + s_i));
-        C.inc(RT_OP_SAMPLES);
-        d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
-        double px = fma(Q->rs, (double)s_i + rnd(g), -0.5);
-        double py = fma(Q->rs, (double)s_j + rnd(g), -0.5);
-        d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
-        d3 origin = karr3(Q->center);
-        if (Q->defocus) {
-          for (;;) {
-            double dx = rnd_pm1(g);
-            double dy = rnd_pm1(g);
-            if (fma(dx, dx, dy * dy) < 1.0) {
-              const kparams_t R = kparams();
-              origin = vfma(dy, karr3(R->ddv), vfma(dx, karr3(R->ddu), karr3(R->center)));
-              break;
-            }
-          }
-        }
-        ro = origin;
-        rd = ps - origin;
-        tm = rnd(g);
-        beta = mk(1., 1., 1.);
-        Lp = mk(0., 0., 0.);
-        depth = P.max_depth;
-        alive = true;
-      }
-    }
-    next += __popcll(want);
-    if (__ballot(alive) == 0ull) {
-      if (!more) break;
-      continue;
-    }
-    if (!alive) continue;
-    if (depth <= 0) {  // ray_color depth guard render.rs:260-262
-      C.inc(RT_OP_DEPTH_CUTOFF);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
-      continue;
-    }
-    C.inc(RT_OP_WORLD_QUERIES);
-    PROF(1);
-#ifdef RT_PROF
-    prof_lanes += __popcll(__ballot(1));
-    prof_iters += 1;
-#endif
-    double t;
-    uint32_t hn = 0;
-    int hf = -1;
-#ifdef RT_ABL_TRAV2  // ablation build: the traversal runs twice (same result); the time delta
-                     // is the traversal's cost
-    {
-      double z = 0.0;
-      asm volatile("" : "+v"(z));
-      double t2;
-      uint32_t hn2;
-      int hf2;
-      traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001 + z,
-                                            INFINITY, t2,
-                                      hn2, hf2, g, C);
-      asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
-    }
-#endif
-    if (!traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001,
-                                               INFINITY, t, hn, hf, g, C)) {
-      C.inc(RT_OP_MISSES);  // background render.rs:298-309
-      Lp = Lp + beta * karr3(kparams()->bg);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
-      continue;
-    }
-    // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
-    PROF(2);
-    const uint32_t* X = T.nodes + hn;
-    uint32_t type = X[0] & 0xffu;
-    d3 o, d;
-    frame_ray(T.nodes, hf, ro, rd, o, d);
-    d3 p = vfma(t, d, o);
-    d3 normal;
-    bool front = true;
-    double u = 0., v = 0.;
-    const uint32_t* M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
-    uint4 mh = ld4u(M);
-    const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
-    if (type == RTL_QUAD) {
-      const gptr XG = X + RTL_QUAD_GEN;
-      d3 n = ld3(XG, 0);
-      front = dot(d, n) < 0.0;  // set_face_normal hittable.rs:22-37
-      normal = front ? n : -n;
-      if (needs_uv) {
-        d3 pq = p - ld3(XG, 4);
-        u = dot(pq, ld3(XG, 8));
-        v = dot(pq, ld3(XG, 12));
-      }
-    } else if (type == RTL_SPHERE) {
-      d3 c = ld3(X, 0);
-      if (X[3]) c = vfma(tm, ld3(X, 4), c);
-      d3 outward = (p - c) * ldd(X, 7);
-      front = dot(d, outward) < 0.0;
-      normal = front ? outward : -outward;
-      if (needs_uv) sphere_uv(outward, u, v);
-    } else {  // volume (constant_medium.rs:82-90)
-      normal = mk(1., 0., 0.);
-    }
-    if (hf >= 0) {  // back to world space, innermost transform first
-      uint4 fh = ld4u(T.nodes + hf);
-      uint4 ch = ld4u(T.nodes + hf + 4);
-      const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-      for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
-        if ((uint32_t)k < fh.z) xform_out(T.nodes + c4[k], p, normal);
-    }
-    const uint32_t kind = mh.x & 0xffu;
-    PROF(3);
-    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
-      C.inc(RT_OP_EMISSIVE_HITS);
-      if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
-      continue;
-    }
-    if (kind == RT_MAT_METAL) {  // material.rs:124-134
-      C.inc(RT_OP_METAL);
-      d3 reflected = reflect(unit_vector(rd), normal);
-      d3 ruv = random_unit_vector(g);
-      reflected = vfma(ldd(M, 3), ruv, unit_vector(reflected));
-      beta = beta * ld3(M, 0);
-      ro = p;
-      rd = reflected;
-      --depth;
-      continue;
-    }
-    if (kind == RT_MAT_DIELECTRIC) {  // material.rs:166-191
-      C.inc(RT_OP_DIELECTRIC);
-      double ratio = front ? ldd(M, 4) : ldd(M, 3);  // 1/ir : ir
-      d3 ud = unit_vector(rd);
-      double cos_t = fmin(dot(-ud, normal), 1.0);
-      double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
-      bool refl = ratio * sin_t > 1.0;
-      if (!refl) {
-        double r0 = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
-        double xx = 1.0 - cos_t;
-        double x2 = xx * xx;
-        refl = fma(1.0 - r0, x2 * x2 * xx, r0) > rnd(g);
-      }
-      rd = refl ? reflect(ud, normal) : refract(ud, normal, ratio);
-      beta = beta * ld3(M, 0);
-      ro = p;
-      --depth;
-      continue;
-    }
-    // Lambertian / Isotropic: mixture-PDF branch render.rs:278-292
-    PROF(4);
-    const bool iso = kind == RT_MAT_ISOTROPIC;
-    C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
-    d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
-    // Draw order as the reference: mixture coin (pdf.rs:120-126), then light index
-    // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
-    bool light_branch = false;
-    if (have_lights) light_branch = rnd(g) < 0.5;
-    uint32_t ltype = 0;
-    gptr L = T.lights;
-    if (light_branch) {
-      C.inc(RT_OP_LIGHT_GEN);
-      uint32_t li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
-      L = T.lights + T.loffs[li];
-      ltype = L[0] & 0xffu;
-    } else {
-      C.inc(RT_OP_COSINE_GEN);
-    }
-    d3 dir;
-    const d3 un = unit_vector(normal);  // CosinePDF's w (pdf.rs:58-62, onb.rs:33)
-    if (iso && !light_branch) {
-      dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
-    } else if (light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
-      dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
-    } else {
-      // Quad::random (object.rs:503-506), Sphere::random / random_to_sphere (204-212, 122-132)
-      // and CosinePDF::generate (pdf.rs:75-77, vec3.rs:240-250) share one straight-line block:
-      // one ONB, one sincos, selects instead of divergent branches.
-      const double r1 = rnd(g), r2 = rnd(g);
-      const bool lq = light_branch && ltype == RTL_QUAD;
-      const bool ls = light_branch && ltype == RTL_SPHERE;
-      d3 c = ls ? ld3(L, 0) : p;
-      double rad = ls ? ldd(L, 3) : 0.0;
-      d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
-      double dist2 = dot(wdir, wdir);
-      d3 w = ls ? unit_vector(wdir) : un;
-      d3 aa = fabs(w.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
-      Onb b;
-      b.v = unit_vector(cross(w, aa));
-      b.u = cross(w, b.v);
-      b.w = w;
-      double sn, cs;
-      sincos2pi(r1, &sn, &cs);
-      double z, rho;
-      if (ls) {
-        z = fma(r2, sqrt(1.0 - rad * rad / dist2) - 1.0, 1.0);
-        rho = sqrt(fma(-z, z, 1.0));
-      } else {
-        z = sqrt(1.0 - r2);
-        rho = sqrt(r2);
-      }
-      d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
-      if (lq) {
-        local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
-      }
-      dir = local;
-    }
-    double mat_pdf, s_pdf;
-    if (iso) {
-      mat_pdf = 1.0 / (4.0 * kPi);                   // SpherePDF::value pdf.rs:47-49
-      s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
-    } else {
-      d3 udir = unit_vector(dir);
-      double cv = dot(udir, un) / kPi;               // CosinePDF::value pdf.rs:69-73
-      mat_pdf = cv > 0.0 ? cv : 0.0;
-      double cs = dot(normal, udir);                 // Lambertian::scattering_pdf 100-108
-      s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
-    }
-    double pdf_val = mat_pdf;
-    PROF(5);
-#ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
-    if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, C), 0.5 * mat_pdf);  // pdf.rs:116
-#endif
-    PROF(6);
-    beta = beta * (atten * (s_pdf / pdf_val));
-    ro = p;
-    rd = dir;
-    --depth;
-  }
-#ifdef RT_PROF
-  PROF(7);
-  if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(&P.ops[k], prof_acc[k]);
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&P.ops[8], prof_lanes);
-    atomicAdd(&P.ops[9], prof_iters);
-  }
-#endif
-#undef PROF
-  if (COUNT) {
-    C.flush(sh_ops);
-    __syncthreads();
-    for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x)
-      if (sh_ops[k]) atomicAdd(&P.ops[k], (unsigned long long)sh_ops[k]);
-  }
+  trace_body<COUNT, VOL, TEX, BVH, TravInterp>(P);
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
