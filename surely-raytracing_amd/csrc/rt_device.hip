@@ -39,7 +39,8 @@ namespace {
 
 // Ahead-of-time kernels: the interpreter traversal, one per feature combination.
 template <bool COUNT, bool VOL, bool TEX, bool BVH>
-__global__ __launch_bounds__(kBlock, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(TraceParams P) {
+__global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(
+    TraceParams P) {
   trace_body<COUNT, VOL, TEX, BVH, TravInterp>(P);
 }
 
@@ -124,6 +125,7 @@ struct rt_scene {
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
   int resident_blocks[16] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
+  size_t resident_lds[16] = {};  // ... at this dynamic LDS size
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -172,8 +174,9 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   // aligned; texels last (never staged).
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   size_t o_nodes = 0, s_nodes = F.nodes.size() * 4;
-  // +64 B: the LANE walker fetches 64 bytes of every node it visits, END (16 B) included
-  size_t o_mats = al(o_nodes + s_nodes + 64), s_mats = F.mats.size() * 4;
+  // +256 B: the LANE walker fetches 64 bytes of every node it visits (END, 16 B, included) and
+  // prefetches one quad record past a batch
+  size_t o_mats = al(o_nodes + s_nodes + 256), s_mats = F.mats.size() * 4;
   size_t o_texs = al(o_mats + s_mats), s_texs = F.texs.size() * 4;
   size_t o_lig = al(o_texs + s_texs), s_lig = F.lights.size() * 4;
   size_t o_loff = al(o_lig + s_lig), s_loff = F.light_offs.size() * 4;
@@ -319,12 +322,24 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     P.stage_src = sc->perlin;
     P.stage_bytes = P.n_perlin_lds * RTL_PERLIN_BYTES;
   }
+  // BVH region (rt_layout.h): in LDS with the small scene, else staged after the Perlin tables
+  // as far as the LDS budget of the 512-thread BVH workgroup allows (the rest is read from HBM)
+  P.bvh_words = sc->hdr.bvh_words;
+  if (P.stage_scene) {
+    P.bvh_lds_words = P.bvh_words;
+    P.bvh_lds_off = 0;
+  } else if (sc->hdr.has_bvh) {
+    const size_t room = kLdsBvhMax > P.stage_bytes ? kLdsBvhMax - P.stage_bytes : 0;
+    P.bvh_lds_words = (uint32_t)std::min<size_t>(P.bvh_words, room / 64 * 16);
+    P.bvh_lds_off = P.stage_bytes;
+  }
   P.o_mats = sc->o_mats;
   P.o_texs = sc->o_texs;
   P.o_lights = sc->o_lights;
   P.o_loffs = sc->o_loffs;
   P.o_perl = sc->o_perl;
-  const size_t lds_bytes = P.stage_bytes;
+  const size_t lds_bytes =
+      P.stage_bytes + (P.stage_scene ? 0u : (size_t)P.bvh_lds_words * 4u);
   for (int k = 0; k < 3; ++k) {
     P.center[k] = cam->center[k];
     P.p00[k] = cam->pixel00_loc[k];
@@ -373,13 +388,18 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
                    (bvh ? 1 : 0);
   kern_t kern = table[kidx];
-  if (sc->resident_blocks[kidx] == 0) {
+  const int block = bvh ? kBlockBvh : kBlock;
+  if (lds_bytes > (64u << 10))
+    HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_bytes));
+  if (sc->resident_blocks[kidx] == 0 || sc->resident_lds[kidx] != lds_bytes) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kBlock, lds_bytes) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, block, lds_bytes) !=
             hipSuccess ||
         nb <= 0)
       nb = 1;
     sc->resident_blocks[kidx] = nb;
+    sc->resident_lds[kidx] = lds_bytes;
   }
   const int64_t max_blocks = (int64_t)sc->resident_blocks[kidx] * std::max(1, sc->n_cu);
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
@@ -389,11 +409,11 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     P.n_pools = (int)(waves_per_sj * cn);
     // persistent grid: as many waves as the device holds at once (never more than pools)
     const int64_t blocks =
-        std::min(max_blocks, (waves_per_sj * cn + (kBlock / 64) - 1) / (kBlock / 64));
+        std::min(max_blocks, (waves_per_sj * cn + (block / 64) - 1) / (block / 64));
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
     const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), lds_bytes, stream, P);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sc->tev[ring][1], stream));
     sc->tev_render[ring] = sc->n_render;

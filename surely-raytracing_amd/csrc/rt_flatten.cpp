@@ -113,6 +113,26 @@ std::unique_ptr<Node> read_node(Reader& r, int depth) {
   return nd;
 }
 
+// Structural equality of two object subtrees (the blob serialises a BvhNode's span-1 leaf
+// (obj, obj), hittable.rs:161-162, as two copies of the same subtree).
+bool same_tree(const Node& a, const Node& b) {
+  if (a.tag != b.tag || a.mat != b.mat || a.moving != b.moving || a.kids.size() != b.kids.size())
+    return false;
+  if (std::memcmp(a.f, b.f, sizeof(a.f)) != 0 || std::memcmp(a.bbox, b.bbox, sizeof(a.bbox)) != 0)
+    return false;
+  for (size_t k = 0; k < a.kids.size(); ++k)
+    if (!same_tree(*a.kids[k], *b.kids[k])) return false;
+  return true;
+}
+// ConstantMedium draws a random number per boundary crossing (constant_medium.rs:75): a
+// subtree holding one is not deterministic in its interval, so it is never elided.
+bool has_volume_node(const Node& a) {
+  if (a.tag == RT_OBJ_VOLUME) return true;
+  for (auto& k : a.kids)
+    if (has_volume_node(*k)) return true;
+  return false;
+}
+
 // write an f64 payload value at double index k of the node starting at word p
 inline void putd(std::vector<uint32_t>& w, size_t p, int k, double d) {
   std::memcpy(&w[p + 4 + 2 * (size_t)k], &d, 8);
@@ -207,7 +227,7 @@ struct Emitter {
     size_t p = push(RTL_SPHERE, RTL_SPHERE_WORDS);
     const double* f = n.f;  // c 0-2, radius 3, cvec 4-6
     w[p + 2] = (uint32_t)(n.mat < 0 ? 0 : n.mat);
-    w[p + 3] = n.moving ? 1u : 0u;
+    if (n.moving) w[p] |= RTL_SPHERE_MOVING;
     putd(w, p, 0, f[0]), putd(w, p, 1, f[1]), putd(w, p, 2, f[2]), putd(w, p, 3, f[3]);
     putd(w, p, 4, f[4]), putd(w, p, 5, f[5]), putd(w, p, 6, f[6]);
     putd(w, p, 7, 1.0 / f[3]);  // outward = (p - c) * (1/r)
@@ -253,7 +273,13 @@ struct Emitter {
         size_t p = push(RTL_BVH, RTL_BVH_WORDS);
         for (int k = 0; k < 6; ++k) putd(w, p, k, n.bbox[k]);
         emit(*n.kids[0], frame, chain, in_volume);
-        emit(*n.kids[1], frame, chain, in_volume);
+        if (same_tree(*n.kids[0], *n.kids[1]) && !has_volume_node(*n.kids[1])) {
+          size_t d = push(RTL_DUP, RTL_DUP_WORDS);
+          emit(*n.kids[1], frame, chain, in_volume);
+          set_skip(d);
+        } else {
+          emit(*n.kids[1], frame, chain, in_volume);
+        }
         set_skip(p);
         break;
       }
@@ -307,6 +333,58 @@ bool tex_needs_uv(const std::vector<uint32_t>& texs, uint32_t id, int depth) {
   if (t[0] == RT_TEX_IMAGE) return t[1] > 0 && t[2] > 0;
   if (t[0] == RT_TEX_CHECKER) return tex_needs_uv(texs, t[1], depth + 1) || tex_needs_uv(texs, t[2], depth + 1);
   return false;
+}
+
+// Words of the record starting with header word h.
+uint32_t record_words(uint32_t h) {
+  switch (h & 0xffu) {
+    case RTL_QUAD: return RTL_QUAD_WORDS;
+    case RTL_SPHERE: return RTL_SPHERE_WORDS;
+    case RTL_BVH: return RTL_BVH_WORDS;
+    case RTL_TRANSLATE:
+    case RTL_ROTATE_Y: return RTL_XFORM_WORDS;
+    case RTL_EXIT: return RTL_EXIT_WORDS;
+    case RTL_VOLUME: return RTL_VOLUME_WORDS;
+    case RTL_DUP: return RTL_DUP_WORDS;
+    default: return 4;  // END, QUADS header
+  }
+}
+
+// Move every BVH record to the front of the node array (the BVH region [0, bvh_words), staged
+// in LDS by rt_trace) and make every link explicit (rt_layout.h): BVH records get their first
+// child in word 2, every other record its pre-order successor in word 3. The visiting order,
+// and with it every result, is unchanged: only the addresses move.
+void relocate(std::vector<uint32_t>& w, uint32_t* root, uint32_t* bvh_words) {
+  std::vector<size_t> pos;
+  for (size_t p = 0; p < w.size(); p += record_words(w[p])) pos.push_back(p);
+  std::vector<uint32_t> map(w.size() + 1, 0xffffffffu);
+  uint32_t nb = 0;
+  for (size_t p : pos)
+    if ((w[p] & 0xffu) == RTL_BVH) map[p] = nb, nb += RTL_BVH_WORDS;
+  uint32_t nm = nb;
+  for (size_t p : pos)
+    if ((w[p] & 0xffu) != RTL_BVH) map[p] = nm, nm += record_words(w[p]);
+  map[w.size()] = nm;
+  auto m = [&](uint32_t old) { return old == 0xffffffffu ? old : map[old]; };
+  std::vector<uint32_t> out(w.size(), 0u);
+  for (size_t p : pos) {
+    const uint32_t h = w[p], sz = record_words(h), q = map[p];
+    std::memcpy(&out[q], &w[p], sz * 4);
+    const uint32_t type = h & 0xffu;
+    if (type != RTL_QUAD && type != RTL_SPHERE && type != RTL_EXIT && type != RTL_END)
+      out[q + 1] = m(w[p + 1]);  // skip
+    if (type == RTL_BVH) {
+      out[q + 2] = m((uint32_t)(p + sz));  // first child
+    } else if (type != RTL_END) {
+      out[q + 3] = m((uint32_t)(p + sz));  // pre-order successor
+    }
+    if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y)
+      for (uint32_t k = 0; k < w[p + 2]; ++k) out[q + 4 + k] = m(w[p + 4 + k]);  // chain
+    if (type == RTL_EXIT) out[q + 2] = m(w[p + 2]);  // parent frame
+  }
+  w.swap(out);
+  *root = m(*root);
+  *bvh_words = nb;
 }
 
 }  // namespace
@@ -480,6 +558,8 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
     *err = em.err;
     return em.status;
   }
+  uint32_t root = 0, bvh_words = 0;
+  relocate(F.nodes, &root, &bvh_words);
   if (F.nodes.size() >= 0x7fffffffu) {
     *err = "scene too large";
     return RT_ERR_UNSUPPORTED;
@@ -520,7 +600,8 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   }
   if (blob->n_texels) F.texels.assign(blob->texels, blob->texels + blob->n_texels);
   rtl_scene_header& h = F.hdr;
-  h.root = 0;
+  h.root = root;
+  h.bvh_words = bvh_words;
   h.n_node_words = (uint32_t)F.nodes.size();
   h.n_mats = (uint32_t)n_mat;
   h.n_texs = (uint32_t)n_tex;

@@ -36,6 +36,15 @@ struct cond<false, T, F> {
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 constexpr int kBlock = 256;   // 4 waves per workgroup
+// BVH kernels run two waves per SIMD (MinWaves below) in ONE 512-thread workgroup per CU, so the
+// workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH region (rt_layout.h).
+constexpr int kBlockBvh = 512;
+template <bool BVH>
+struct BlockOf {
+  static constexpr int value = BVH ? kBlockBvh : kBlock;
+};
+// Dynamic LDS budgets: whole small scenes (kStageScene) / the BVH region of a BVH kernel.
+constexpr size_t kLdsBvhMax = 152u << 10;
 // Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument). 4 caps the
 // allocation at 128 VGPRs. Kernels with a per-lane BVH walker need more than that without
 // spilling inside the walk, and spills there cost more than the occupancy they buy: 2 waves
@@ -178,6 +187,10 @@ struct TraceParams {
   // n_perlin_lds Perlin tables are copied. Offsets are bytes from the start of the allocation.
   const uint8_t* stage_src;
   uint32_t stage_bytes, stage_scene;
+  // BVH region (rt_layout.h): node words [0, bvh_words) are BVH records; the first bvh_lds_words
+  // of them are in LDS at byte offset bvh_lds_off (staged by the prologue unless stage_scene
+  // already copied the node array)
+  uint32_t bvh_words, bvh_lds_words, bvh_lds_off;
   uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
@@ -361,7 +374,7 @@ __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double
   C.inc(RT_OP_SPHERE_TESTS);
   d3 center = ld3(s, 0);
   double r = ldd(s, 3);
-  if (s[3]) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
+  if (s[0] & RTL_SPHERE_MOVING) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
   d3 oc = o - center;
   double a = dot(d, d);
   double half_b = dot(oc, d);
@@ -402,6 +415,25 @@ __device__ __forceinline__ bool aabb_hit(const double (&mn)[3], const double (&m
   return true;
 }
 
+// The same test without branches: tmin only grows and tmax only shrinks, so one final
+// comparison answers the reference's per-axis early exit, and max/min (IEEE maxNum/minNum:
+// a NaN slab bound, (min - o) * inf with o on the slab plane, leaves the interval alone) are
+// the reference's `if t0 > tmin { tmin = t0 }` / `if t1 < tmax { tmax = t1 }` (ties differ
+// at most in the sign of a zero, which no comparison sees).
+__device__ __forceinline__ bool aabb_hit_bf(const double (&mn)[3], const double (&mx)[3], d3 o,
+                                            d3 inv, double tmin, double tmax) {
+  const double oo[3] = {o.x, o.y, o.z}, id[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double t0 = (mn[a] - oo[a]) * id[a];
+    const double t1 = (mx[a] - oo[a]) * id[a];
+    const bool neg = id[a] < 0.0;
+    tmin = __builtin_fmax(tmin, neg ? t1 : t0);
+    tmax = __builtin_fmin(tmax, neg ? t0 : t1);
+  }
+  return tmin < tmax;
+}
+
 // Translate/RotateY ray into object space (transform.rs:59, 86-107).
 template <class Ptr>
 __device__ __forceinline__ void xform_in(Ptr X, d3& o, d3& d) {
@@ -437,6 +469,18 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
     if ((uint32_t)k < h.z) xform_in(N + c4[k], o, d);
 }
 
+#ifdef RT_PROF
+// profiling build: per-lane LANE-walker step counts and per-workgroup traversal counters
+// (flushed to P.ops[10..17] at kernel exit; tools_gpu/prof_sections.py)
+__shared__ uint32_t prof_steps[kBlockBvh];
+__shared__ unsigned long long prof_trav[16];
+__shared__ uint32_t prof_wmax[kBlockBvh / 64];
+__device__ __forceinline__ bool prof_first_lane() {
+  const unsigned long long m = __ballot(1);
+  return (threadIdx.x & 63) == (unsigned)(__builtin_ctzll(m));
+}
+#endif
+
 // ---------------------------------------------------------------- traversal
 // Threaded walk of the flattened scene (rt_layout.h). MAIN: the world (records the hit node and
 // its frame, handles ConstantMedium when VOL). !MAIN: a volume boundary (closest t only).
@@ -460,34 +504,76 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
   const Ptr N = (Ptr)P.nodes;
   double closest = tmax;
   bool hit = false;
+  // 1/d of the lane's ray in the current frame (Aabb::hit object.rs:347 divides per test; the
+  // quotient is the same IEEE value every time, so the LANE walker divides once per frame)
   d3 inv = mk(0., 0., 0.);
-  bool inv_ok = false;
+  if (!UNI) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+#ifdef RT_PROF
+  unsigned long long pf_inner = 0, pf_leaf = 0, pf_outer_n = 0, pf_inner_n = 0;
+  unsigned long long pf_t = __builtin_readcyclecounter();
+#endif
   for (;;) {
     uint4 h, q1, q2, q3;
+#ifdef RT_PROF
+    if (!UNI) {
+      const unsigned long long now = __builtin_readcyclecounter();
+      pf_leaf += now - pf_t;
+      pf_t = now;
+      pf_outer_n += 1;
+    }
+#endif
     if (UNI) {
       node = __builtin_amdgcn_readfirstlane(node);
       frame = __builtin_amdgcn_readfirstlane(frame);
       h = ld4u(N + node);
     } else {
       if (node == stop) break;
-      // speculative 64-byte fetch (the node array is padded past its END)
-      ld64(N + node, h, q1, q2, q3);
       // while-while: a lane steps through BVH nodes until it reaches a leaf (or the subtree's
       // end); lanes that got there first wait at the loop exit, so the leaf bodies below run
-      // with every lane that has a leaf instead of interleaving with the AABB steps.
-      while ((h.x & 0xffu) == RTL_BVH) {
+      // with every lane that has a leaf instead of interleaving with the AABB steps. BVH records
+      // live in the BVH region [0, bvh_words) (rt_layout.h), so the index alone says "BVH node"
+      // and no header is read; the region's first bvh_lds_words words are staged in LDS.
+      const kparams_t KP = kparams();
+      const uint32_t bvh_words = KP->bvh_words, bvh_lds = KP->bvh_lds_words;
+      const uint4* LB = reinterpret_cast<const uint4*>(rt_lds + KP->bvh_lds_off);
+      auto step = [&](uint4 bh, uint4 b1, uint4 b2, uint4 b3) {
         C.inc(RT_OP_AABB_TESTS);
-        if (!inv_ok) {
-          inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-          inv_ok = true;
+#ifdef RT_PROF
+        prof_steps[threadIdx.x] += 1;
+        pf_inner_n += 1;
+#endif
+        const double mn[3] = {hilo(b1.x, b1.y), hilo(b2.x, b2.y), hilo(b3.x, b3.y)};
+        const double mx[3] = {hilo(b1.z, b1.w), hilo(b2.z, b2.w), hilo(b3.z, b3.w)};
+        node = aabb_hit_bf(mn, mx, o, inv, tmin, closest) ? bh.z : bh.y;  // first child : skip
+      };
+      if (bvh_lds == bvh_words) {  // the whole region is in LDS
+        while (node < bvh_words) {
+          const uint4* L = LB + (node >> 2);
+          step(L[0], L[1], L[2], L[3]);
+          if (node == stop) break;
         }
-        const double mn[3] = {hilo(q1.x, q1.y), hilo(q2.x, q2.y), hilo(q3.x, q3.y)};
-        const double mx[3] = {hilo(q1.z, q1.w), hilo(q2.z, q2.w), hilo(q3.z, q3.w)};
-        node = aabb_hit(mn, mx, o, inv, tmin, closest) ? node + RTL_BVH_WORDS : h.y;
-        if (node == stop) break;
-        ld64(N + node, h, q1, q2, q3);
+      } else {
+        while (node < bvh_words) {
+          uint4 bh, b1, b2, b3;
+          if (node < bvh_lds) {
+            const uint4* L = LB + (node >> 2);
+            bh = L[0], b1 = L[1], b2 = L[2], b3 = L[3];
+          } else {
+            ld64(N + node, bh, b1, b2, b3);
+          }
+          step(bh, b1, b2, b3);
+          if (node == stop) break;
+        }
       }
+#ifdef RT_PROF
+      {
+        const unsigned long long now = __builtin_readcyclecounter();
+        pf_inner += now - pf_t;
+        pf_t = now;
+      }
+#endif
       if (node == stop) break;
+      ld64(N + node, h, q1, q2, q3);  // a leaf record (the node array is padded past its END)
     }
     const Ptr X = N + node;
     uint32_t type = h.x & 0xffu;
@@ -510,14 +596,22 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
           hit_frame = frame;
         }
       }
-      node += RTL_QUAD_WORDS;
+      node = h.w;
     } else if (type == RTL_QUADS) {
       // batch of sibling quads: the same sequential closest-hit updates as the list
       const uint32_t cnt = h.x >> 8;
       Ptr Q = X + 4;
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
       uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
+#ifdef RT_EXP_PF2
+      uint4 b0, b1, b2, b3;
+      if (!UNI) {
+        ld64(Q, a0, a1, a2, a3);
+        ld64(Q + RTL_QUAD_WORDS, b0, b1, b2, b3);
+      }
+#else
       if (!UNI) ld64(Q, a0, a1, a2, a3);
+#endif
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
         double t;
         bool hq;
@@ -526,7 +620,12 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         } else {
           const AQuad q = {a0.x, hilo(a1.x, a1.y), hilo(a1.z, a1.w), hilo(a2.x, a2.y),
                            hilo(a2.z, a2.w), hilo(a3.x, a3.y)};
+#ifdef RT_EXP_PF2
+          a0 = b0, a1 = b1, a2 = b2, a3 = b3;
+          ld64(Q + 2 * RTL_QUAD_WORDS, b0, b1, b2, b3);  // two quads ahead (padding covers it)
+#else
           ld64(Q + RTL_QUAD_WORDS, a0, a1, a2, a3);  // past the batch: the next node (padded)
+#endif
           hq = aquad_dispatch<COUNT>(q, Q, o, d, r, tmin, closest, t, C);
         }
         if (hq) {
@@ -549,15 +648,38 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
           hit_frame = frame;
         }
       }
-      node += RTL_SPHERE_WORDS;
+      node = h.w;
     } else if (type == RTL_BVH) {
       if (UNI) {
         if (BVH) {  // the subtree [node, skip) per lane, continuing this walk's closest hit
           double t;
           uint32_t hn;
           int hf;
-          if (traverse<MAIN, COUNT, VOL, false, BVH>(P, node, h.y, wo, wd, tm, o, d, frame, tmin,
-                                                     closest, t, hn, hf, g, C)) {
+#ifdef RT_PROF
+          const unsigned long long pt0 = __builtin_readcyclecounter();
+          prof_steps[threadIdx.x] = 0u;
+#endif
+          const bool sub = traverse<MAIN, COUNT, VOL, false, BVH>(P, node, h.y, wo, wd, tm, o, d,
+                                                                 frame, tmin, closest, t, hn, hf,
+                                                                 g, C);
+#ifdef RT_PROF
+          {
+            const unsigned long long dt = __builtin_readcyclecounter() - pt0;
+            const uint32_t st = prof_steps[threadIdx.x];
+            const int wv = threadIdx.x >> 6;
+            atomicMax(&prof_wmax[wv], st);
+            const uint32_t mx = prof_wmax[wv];
+            const int which = MAIN ? (frame < 0 ? 0 : 1) : 2;
+            if (prof_first_lane()) {
+              prof_wmax[wv] = 0u;
+              atomicAdd(&prof_trav[which], dt);
+              atomicAdd(&prof_trav[3 + (which > 0 ? 1 : 0)], (unsigned long long)mx);
+            }
+            atomicAdd(&prof_trav[5 + (which > 0 ? 1 : 0)], (unsigned long long)st);
+            if (prof_first_lane()) atomicAdd(&prof_trav[7], 1ull);
+          }
+#endif
+          if (sub) {
             closest = t;
             hit = true;
             if (MAIN) {
@@ -571,14 +693,14 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
     } else if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y) {
       C.inc(type == RTL_TRANSLATE ? RT_OP_TRANSLATE : RT_OP_ROTATE_Y);
       xform_in(X, o, d);
-      if (type == RTL_ROTATE_Y) inv_ok = false;
+      if (!UNI && type == RTL_ROTATE_Y) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
       frame = (int)node;
-      node += RTL_XFORM_WORDS;
+      node = h.w;  // the instance's child
     } else if (type == RTL_EXIT) {
       frame = (int)h.z;
       frame_ray(N, frame, wo, wd, o, d);
-      inv_ok = false;
-      node += RTL_EXIT_WORDS;
+      if (!UNI) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+      node = h.w;
     } else if (MAIN && VOL && type == RTL_VOLUME) {
       // ConstantMedium::hit constant_medium.rs:41-95
       C.inc(RT_OP_VOLUME_TESTS);
@@ -591,7 +713,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         double tb;
         uint32_t dn;
         int df;
-        both = traverse<false, COUNT, false, UNI, BVH>(P, node + RTL_VOLUME_WORDS, ~0u, wo, wd, tm,
+        both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
                                                        o, d, frame,
                                                        pass ? t1 + 0.0001 : -kInf, kInf,
                                                        tb, dn, df, g, C);
@@ -615,12 +737,25 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         }
       }
       node = h.y;
+    } else if (type == RTL_DUP) {
+      node = COUNT ? h.w : h.y;
     } else if (type == RTL_END) {
       break;
     } else {
       node = h.y;
     }
   }
+#ifdef RT_PROF
+  if (!UNI) {
+    pf_leaf += __builtin_readcyclecounter() - pf_t;
+    if (prof_first_lane()) {
+      atomicAdd(&prof_trav[8], pf_inner);
+      atomicAdd(&prof_trav[9], pf_leaf);
+      atomicAdd(&prof_trav[10], pf_outer_n);
+      atomicAdd(&prof_trav[11], pf_inner_n);
+    }
+  }
+#endif
   t_out = closest;
   return hit;
 }
@@ -832,11 +967,18 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
     __syncthreads();
   }
-  if (P.stage_bytes) {  // copy the small tables (or just the Perlin tables) into LDS
+  if (P.stage_bytes || (BVH && !P.stage_scene && P.bvh_lds_words)) {
+    // copy the small tables (or just the Perlin tables) into LDS, then the BVH region
     const uint4* src = reinterpret_cast<const uint4*>(P.stage_src);
     uint4* dst = reinterpret_cast<uint4*>(rt_lds);
     const uint32_t n16 = P.stage_bytes / 16;
     for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    if (BVH && !P.stage_scene) {
+      const uint4* bsrc = reinterpret_cast<const uint4*>(P.nodes);
+      uint4* bdst = reinterpret_cast<uint4*>(rt_lds + P.bvh_lds_off);
+      const uint32_t b16 = P.bvh_lds_words / 4;
+      for (uint32_t k = threadIdx.x; k < b16; k += blockDim.x) bdst[k] = bsrc[k];
+    }
     __syncthreads();
   }
   Tabs T;
@@ -850,6 +992,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     T.perlin = rt_lds + (P.stage_scene ? P.o_perl : 0u);
   }
   Ctr<COUNT> C;
+#ifdef RT_PROF
+  if (threadIdx.x < 16) prof_trav[threadIdx.x] = 0ull;
+  if (threadIdx.x < kBlockBvh / 64) prof_wmax[threadIdx.x] = 0u;
+  __syncthreads();
+#endif
 #ifdef RT_PROF  // profiling build: wave cycles per loop section into P.ops[0..7] (not shipped)
   unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long prof_last = __builtin_readcyclecounter();
@@ -1027,7 +1174,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       }
     } else if (type == RTL_SPHERE) {
       d3 c = ld3(X, 0);
-      if (X[3]) c = vfma(tm, ld3(X, 4), c);
+      if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
       d3 outward = (p - c) * ldd(X, 7);
       front = dot(d, outward) < 0.0;
       normal = front ? outward : -outward;
@@ -1170,6 +1317,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     atomicAdd(&P.ops[8], prof_lanes);
     atomicAdd(&P.ops[9], prof_iters);
   }
+  __syncthreads();
+  if (threadIdx.x < 16) atomicAdd(&P.ops[10 + threadIdx.x], prof_trav[threadIdx.x]);
 #endif
 #undef PROF
   if (COUNT) {

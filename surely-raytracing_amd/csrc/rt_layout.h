@@ -15,6 +15,13 @@
 // own closest-hit state (constant_medium.rs:46-55).
 //
 // Word = 4 bytes; node offsets are word indices; every node starts 16-byte aligned.
+//
+// Addresses vs order (rt_flatten.cpp relocate): after emission every BVH record is moved to
+// the front, the BVH region [0, bvh_words), which rt_trace stages in LDS; the other records
+// keep their relative order after it. Links are therefore explicit: a BVH record holds its
+// first child in word 2 (its skip in word 1), every other record its pre-order successor in
+// word 3 ("next": where the walk continues after a primitive, and the child of an instance,
+// volume or DUP). Quads of a QUADS batch stay contiguous.
 #pragma once
 #include <stdint.h>
 
@@ -29,10 +36,16 @@
 #define RTL_OTHER 8 /* light entry whose pdf_value is 0 (Object default arm, object.rs:295-311) */
 #define RTL_QUADS 9 /* batch of consecutive sibling quads: header word 0 = type | count << 8, then
                        `count` QUAD records; traversed in order, exactly like the list it replaces */
+#define RTL_DUP 10  /* the right child of a BvhNode whose two children are the same deterministic
+                       subtree (span-1 leaves, hittable.rs:161-162): [hdr][skip][0][0], then the
+                       subtree. Re-testing it with [t_min, rec.t] (hittable.rs:223-228) reproduces
+                       the left child's record exactly, so the renderer jumps to skip; the
+                       op-counting build walks it, so counts stay the reference's. */
+#define RTL_DUP_WORDS 4
 /* header word 0: type | (flags << 8); word 1: skip (next node after the subtree).
  * Payloads are f64 (the reference computes in f64) starting at word 4, read as
  * 16-byte double2 pairs. dN = double index N counted from word 4. */
-/* QUAD (36 words): [hdr][skip][mat][0] d0-1 n.xy | d2-3 n.z,D | d4-5 q.xy | d6-7 q.z,area |
+/* QUAD (36 words): [hdr][skip][mat][next] d0-1 n.xy | d2-3 n.z,D | d4-5 q.xy | d6-7 q.z,area |
  *   d8-9 A.xy | d10-11 A.z,0 | d12-13 B.xy | d14-15 B.z,0      with A = v x w, B = w x u, so
  *   the planar coordinates of object.rs:469-470, a = w.(pq x v) and b = w.(u x pq), are the
  *   same triple products evaluated as a = pq.A, b = pq.B (two dots instead of two crosses and
@@ -41,7 +54,7 @@
  * (object.rs:503-506). */
 /* World QUAD records (48 words) put an axis-aligned form FIRST, so one 64-byte scalar load
  * covers the header and everything the axis-aligned test reads, and the general payload after it:
- *   [hdr | axis << 8][skip][mat][0] d0-5 q_k, q_lo, C_lo, q_hi, C_hi, 0 | d6-21 general payload
+ *   [hdr | axis << 8][skip][mat][next] d0-5 q_k, q_lo, C_lo, q_hi, C_hi, 0 | d6-21 general payload
  * (the QUAD layout above, read through X + RTL_QUAD_GEN). axis = k + 1 when the quad is
  * axis-aligned in its frame (u along axis i, v along axis j, normal along k; 0 = general). Then
  * n = +-e_k, D = +-q_k, and A, B each have one non-zero component, so the general test's
@@ -53,18 +66,20 @@
 #define RTL_QUAD_WORDS 48
 #define RTL_QUAD_AXIS(h) (((h) >> 8) & 0x3u)
 #define RTL_LQUAD_WORDS 52
-/* SPHERE (20 words): [hdr][skip][mat][moving] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r  object.rs:73-105 */
+/* SPHERE (20 words): [hdr | moving][skip][mat][next] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r
+ *                                                                             object.rs:73-105 */
+#define RTL_SPHERE_MOVING 0x100u
 #define RTL_SPHERE_WORDS 20
-/* BVH (16 words): [hdr][skip][0][0] d0-5 xmin xmax ymin ymax zmin zmax     hittable.rs:135-187 */
+/* BVH (16 words): [hdr][skip][child][0] d0-5 xmin xmax ymin ymax zmin zmax  hittable.rs:135-187 */
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
- *   [hdr][skip][chain_len][0] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
+ *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
  *   translate: p = offset.xyz; rotate_y: p0 = sin, p1 = cos                  transform.rs */
 #define RTL_XFORM_WORDS 16
 #define RTL_MAX_CHAIN 4
-/* EXIT (4 words): [hdr][skip=unused][parent frame node or -1][0] */
+/* EXIT (4 words): [hdr][skip=unused][parent frame node or -1][next] */
 #define RTL_EXIT_WORDS 4
-/* VOLUME (8 words): [hdr][skip][mat][0] d0 neg_inv_density, d1 0; the boundary follows and an
+/* VOLUME (8 words): [hdr][skip][mat][next] d0 neg_inv_density, d1 0; the boundary follows and an
  * END node terminates it                                                    constant_medium.rs */
 #define RTL_VOLUME_WORDS 8
 #define RTL_END_WORDS 4
@@ -98,4 +113,5 @@ typedef struct rtl_scene_header {
   uint32_t n_texel_bytes;
   uint32_t pdf_materials; /* any Lambertian / Isotropic                           */
   uint32_t has_textures;  /* a material references a non-solid texture            */
+  uint32_t bvh_words;     /* BVH region: node words [0, bvh_words) hold every BVH record */
 } rtl_scene_header;

@@ -27,3 +27,18 @@ print(f"  lanes alive at traversal: {st.ops[8] / max(1, st.ops[9]):.2f} of 64 "
       f"({st.ops[9]} wave-iterations)")
 for n, c in zip(NAMES, cyc):
     print(f"  {n:24s} {100 * c / cyc.sum():6.2f} %   {c / st.samples:9.1f} wave-cyc/sample")
+o = [st.ops[10 + k] for k in range(16)]
+if o[7]:
+    tot = cyc.sum()
+    print(f"  BVH subtree walks: {o[7]} wave-calls; wave-cycles top-level {100 * o[0] / tot:.1f} %, "
+          f"in-transform {100 * o[1] / tot:.1f} %, volume boundary {100 * o[2] / tot:.1f} %")
+    print(f"  LANE walker node steps: sum-of-lanes top {o[5]}, in-transform {o[6]}; "
+          f"wave max-steps top {o[3]}, in-transform {o[4]}")
+    for nm, s_, m_ in (("top", o[5], o[3]), ("in-transform", o[6], o[4])):
+        if m_:
+            print(f"    {nm}: SIMD efficiency of the AABB steps {s_ / (64.0 * m_):.3f}, "
+                  f"{s_ / st.samples:.2f} lane-steps/sample, {64.0 * m_ / st.samples:.2f} wave-step-slots/sample")
+if o[10]:
+    print(f"  LANE walker (all subtree walks, incl. volume boundaries): inner BVH-step loop "
+          f"{100 * o[8] / tot:.1f} % ({o[11]} wave-iterations, {o[8] / max(1, o[11]):.0f} cyc each), "
+          f"leaf part {100 * o[9] / tot:.1f} % ({o[10]} outer wave-iterations, {o[9] / max(1, o[10]):.0f} cyc each)")
