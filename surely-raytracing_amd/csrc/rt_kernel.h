@@ -475,10 +475,23 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
 __shared__ uint32_t prof_steps[kBlockBvh];
 __shared__ unsigned long long prof_trav[16];
 __shared__ uint32_t prof_wmax[kBlockBvh / 64];
+__shared__ unsigned long long prof_wt[kBlockBvh / 64];
 __device__ __forceinline__ bool prof_first_lane() {
   const unsigned long long m = __ballot(1);
   return (threadIdx.x & 63) == (unsigned)(__builtin_ctzll(m));
 }
+// wave-level section timer of the LANE walker: cycles since the wave's last checkpoint go to
+// section k (prof_trav[8 + k]), and cnt counts the checkpoint (prof_trav[12 + k])
+#define PFW(k, cnt)                                                      \
+  do {                                                                   \
+    const unsigned long long now_ = __builtin_readcyclecounter();       \
+    if (prof_first_lane()) {                                             \
+      const int w_ = threadIdx.x >> 6;                                   \
+      if ((k) >= 0) atomicAdd(&prof_trav[8 + (k)], now_ - prof_wt[w_]); \
+      prof_wt[w_] = now_;                                                \
+      if (cnt) atomicAdd(&prof_trav[12 + ((k) < 0 ? 0 : (k))], 1ull);   \
+    }                                                                    \
+  } while (0)
 #endif
 
 // ---------------------------------------------------------------- traversal
@@ -509,18 +522,12 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
   d3 inv = mk(0., 0., 0.);
   if (!UNI) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
 #ifdef RT_PROF
-  unsigned long long pf_inner = 0, pf_leaf = 0, pf_outer_n = 0, pf_inner_n = 0;
-  unsigned long long pf_t = __builtin_readcyclecounter();
+  if (!UNI) PFW(-1, 0);
 #endif
   for (;;) {
     uint4 h, q1, q2, q3;
 #ifdef RT_PROF
-    if (!UNI) {
-      const unsigned long long now = __builtin_readcyclecounter();
-      pf_leaf += now - pf_t;
-      pf_t = now;
-      pf_outer_n += 1;
-    }
+    if (!UNI) PFW(0, 1);
 #endif
     if (UNI) {
       node = __builtin_amdgcn_readfirstlane(node);
@@ -540,7 +547,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         C.inc(RT_OP_AABB_TESTS);
 #ifdef RT_PROF
         prof_steps[threadIdx.x] += 1;
-        pf_inner_n += 1;
+        if (prof_first_lane()) atomicAdd(&prof_trav[13], 1ull);
 #endif
         const double mn[3] = {hilo(b1.x, b1.y), hilo(b2.x, b2.y), hilo(b3.x, b3.y)};
         const double mx[3] = {hilo(b1.z, b1.w), hilo(b2.z, b2.w), hilo(b3.z, b3.w)};
@@ -566,14 +573,14 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         }
       }
 #ifdef RT_PROF
-      {
-        const unsigned long long now = __builtin_readcyclecounter();
-        pf_inner += now - pf_t;
-        pf_t = now;
-      }
+      PFW(1, 0);
 #endif
       if (node == stop) break;
       ld64(N + node, h, q1, q2, q3);  // a leaf record (the node array is padded past its END)
+#ifdef RT_PROF
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PFW(2, 1);
+#endif
     }
     const Ptr X = N + node;
     uint32_t type = h.x & 0xffu;
@@ -638,6 +645,9 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         }
       }
       node = h.y;
+#ifdef RT_PROF
+      if (!UNI) PFW(3, 1);
+#endif
     } else if (type == RTL_SPHERE) {
       double t;
       if (sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C)) {
@@ -746,15 +756,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
     }
   }
 #ifdef RT_PROF
-  if (!UNI) {
-    pf_leaf += __builtin_readcyclecounter() - pf_t;
-    if (prof_first_lane()) {
-      atomicAdd(&prof_trav[8], pf_inner);
-      atomicAdd(&prof_trav[9], pf_leaf);
-      atomicAdd(&prof_trav[10], pf_outer_n);
-      atomicAdd(&prof_trav[11], pf_inner_n);
-    }
-  }
+  if (!UNI) PFW(0, 0);
 #endif
   t_out = closest;
   return hit;

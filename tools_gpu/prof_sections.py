@@ -38,7 +38,9 @@ if o[7]:
         if m_:
             print(f"    {nm}: SIMD efficiency of the AABB steps {s_ / (64.0 * m_):.3f}, "
                   f"{s_ / st.samples:.2f} lane-steps/sample, {64.0 * m_ / st.samples:.2f} wave-step-slots/sample")
-if o[10]:
-    print(f"  LANE walker (all subtree walks, incl. volume boundaries): inner BVH-step loop "
-          f"{100 * o[8] / tot:.1f} % ({o[11]} wave-iterations, {o[8] / max(1, o[11]):.0f} cyc each), "
-          f"leaf part {100 * o[9] / tot:.1f} % ({o[10]} outer wave-iterations, {o[9] / max(1, o[10]):.0f} cyc each)")
+if o[12]:
+    names = ["leaf dispatch / other leaves", "inner BVH steps", "leaf header load", "QUADS batches"]
+    print("  LANE walker sections (wave-level; profiling waits distort a little):")
+    for k in range(4):
+        print(f"    {names[k]:30s} {100 * o[8 + k] / tot:5.1f} %  count {o[12 + k]:>11d}  "
+              f"{o[8 + k] / max(1, o[12 + k]):8.0f} cyc per count")
