@@ -119,6 +119,7 @@ struct rt_scene {
                  *light_offs = nullptr;
   const uint8_t *perlin = nullptr, *texels = nullptr;
   uint32_t o_mats = 0, o_texs = 0, o_lights = 0, o_loffs = 0, o_perl = 0;  // byte offsets in dev
+  int sphere_light0 = -1;  // first SPHERE light record (TraceParams::sphere_light0)
   uint8_t* work = nullptr;  // per-sample radiance slots + f64 running sums (grown on demand)
   size_t work_bytes = 0;
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
@@ -226,6 +227,12 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   sc->o_lights = (uint32_t)o_lig;
   sc->o_loffs = (uint32_t)o_loff;
   sc->o_perl = (uint32_t)o_perl;
+  sc->sphere_light0 = -1;
+  for (size_t i = 0; i < F.light_offs.size(); ++i)
+    if ((F.lights[F.light_offs[i]] & 0xffu) == RTL_SPHERE) {
+      sc->sphere_light0 = (int)i;
+      break;
+    }
   *out = sc;
   return RT_OK;
 }
@@ -307,6 +314,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.root = sc->hdr.root;
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
+  P.inv_n_lights = sc->hdr.n_lights ? 1.0 / (double)sc->hdr.n_lights : 0.0;
+  P.sphere_light0 = sc->sphere_light0;
   P.flags = opts->flags;
   // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
   // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.

@@ -195,8 +195,8 @@ struct Emitter {
     if (light) {
       putd(w, p, 16, u[0]), putd(w, p, 17, u[1]), putd(w, p, 18, u[2]);
       putd(w, p, 20, v[0]), putd(w, p, 21, v[1]), putd(w, p, 22, v[2]);
-      return;
     }
+    const int ax = light ? RTL_LQUAD_AXIS_D : 0;  // double index of the axis-aligned form
     // axis-aligned fast form (rt_layout.h): only when the exact-zero pattern holds
     auto single = [](const double* x) {
       int nz = -1;
@@ -215,11 +215,13 @@ struct Emitter {
     if (f[15] != nk * f[k]) return;  // D = n.q = n_k q_k
     if (single(A) != i || single(B) != j) return;
     w[p] |= (uint32_t)(k + 1) << 8;
-    putd(w, p, 0, f[k]);
+    putd(w, p, ax + 0, f[k]);
     if (i < j) {
-      putd(w, p, 1, f[i]), putd(w, p, 2, A[i]), putd(w, p, 3, f[j]), putd(w, p, 4, B[j]);
+      putd(w, p, ax + 1, f[i]), putd(w, p, ax + 2, A[i]), putd(w, p, ax + 3, f[j]);
+      putd(w, p, ax + 4, B[j]);
     } else {
-      putd(w, p, 1, f[j]), putd(w, p, 2, B[j]), putd(w, p, 3, f[i]), putd(w, p, 4, A[i]);
+      putd(w, p, ax + 1, f[j]), putd(w, p, ax + 2, B[j]), putd(w, p, ax + 3, f[i]);
+      putd(w, p, ax + 4, A[i]);
     }
   }
   void sphere(const Node& n, bool light) {

@@ -180,6 +180,8 @@ struct TraceParams {
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
   int n_pools;                       // pools of this launch: tiles x n_sj
   uint32_t root, n_lights, lights_is_list, flags;
+  int sphere_light0;    // index of the first SPHERE light record, -1 if none
+  double inv_n_lights;  // 1.0 / n_lights (host IEEE division, hittable.rs:116)
   uint32_t n_perlin_lds;  // Perlin tables readable from LDS (TEX kernels)
   // LDS staging (rt_trace prologue): stage_bytes of the scene allocation starting at stage_src.
   // stage_scene = 1: the whole small-table prefix [nodes .. Perlin] is copied, and per-lane
@@ -905,8 +907,11 @@ __device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 
 
 // Light-list PDF value (HittablePDF::value pdf.rs:91-93 -> HittableList::pdf_value
 // hittable.rs:115-124 -> Quad/Sphere::pdf_value object.rs:492-501, 190-202).
+// cos_sl0: cos_theta_max of the first sphere light at `origin` (object.rs:196), computed once per
+// bounce by the caller and shared with Sphere::random (the same expression, the same bits).
 template <bool COUNT>
-__device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>& C) {
+__device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_sl0,
+                            Ctr<COUNT>& C) {
   double sum = 0.0;
   for (uint32_t i = 0; i < P.n_lights; ++i) {
     const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
@@ -915,7 +920,22 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>&
     if (type == RTL_QUAD) {
       C.inc(RT_OP_LIGHT_PDF_QUAD);
       double t;
-      if (quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C)) {
+      bool hq;
+      const uint32_t axis = RTL_QUAD_AXIS(L[0]);
+      if (axis) {  // axis-aligned form at d24 (rt_layout.h): the world quads' bit-identical test
+        const kdptr A = reinterpret_cast<kdptr>(L + 4) + RTL_LQUAD_AXIS_D;
+        const AQuad q = {L[0], A[0], A[1], A[2], A[3], A[4]};
+        if (axis == 1u) {
+          hq = aquad_test<COUNT, 0>(q, origin, dir, mk(rcp_nr(dir.x), 0., 0.), 0.001, kInf, t, C);
+        } else if (axis == 2u) {
+          hq = aquad_test<COUNT, 1>(q, origin, dir, mk(0., rcp_nr(dir.y), 0.), 0.001, kInf, t, C);
+        } else {
+          hq = aquad_test<COUNT, 2>(q, origin, dir, mk(0., 0., rcp_nr(dir.z)), 0.001, kInf, t, C);
+        }
+      } else {
+        hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
+      }
+      if (hq) {
         double len2 = dot(dir, dir);
         double dist2 = (t * t) * len2;
         double cosine = fabs(dot(dir, ld3(L, 0)) / sqrt(len2));
@@ -925,17 +945,21 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, Ctr<COUNT>&
       C.inc(RT_OP_LIGHT_PDF_SPHERE);
       double t;
       if (sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C)) {
-        d3 c = ld3(L, 0);
-        double r = ldd(L, 3);
-        d3 cmo = c - origin;
-        double cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
+        double cos_max;
+        if ((int)i == P.sphere_light0) {
+          cos_max = cos_sl0;
+        } else {
+          d3 cmo = ld3(L, 0) - origin;
+          double r = ldd(L, 3);
+          cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
+        }
         double solid = 2.0 * kPi * (1.0 - cos_max);
         pv = 1.0 / solid;
       }
     }
     sum = i == 0 ? pv : sum + pv;
   }
-  return P.lights_is_list ? sum * (1.0 / (double)P.n_lights) : sum;
+  return P.lights_is_list ? sum * P.inv_n_lights : sum;  // weight = 1/len (hittable.rs:116)
 }
 
 __device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t slot, d3 L) {
@@ -1240,11 +1264,19 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
     bool light_branch = false;
     if (have_lights) light_branch = rnd(g) < 0.5;
-    uint32_t ltype = 0;
+    uint32_t ltype = 0, li = 0;
     gptr L = T.lights;
+    // cos_theta_max of the first sphere light at p (object.rs:196, 205-207; -1 = none)
+    double cos_sl0 = 0.0;
+    if (P.sphere_light0 >= 0) {
+      const gptr S0 = T.lights + T.loffs[P.sphere_light0];
+      const d3 cmo = ld3(S0, 0) - p;
+      const double r0 = ldd(S0, 3);
+      cos_sl0 = sqrt(1.0 - r0 * r0 / dot(cmo, cmo));
+    }
     if (light_branch) {
       C.inc(RT_OP_LIGHT_GEN);
-      uint32_t li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
+      li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
       L = T.lights + T.loffs[li];
       ltype = L[0] & 0xffu;
     } else {
@@ -1264,9 +1296,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const bool lq = light_branch && ltype == RTL_QUAD;
       const bool ls = light_branch && ltype == RTL_SPHERE;
       d3 c = ls ? ld3(L, 0) : p;
-      double rad = ls ? ldd(L, 3) : 0.0;
       d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
-      double dist2 = dot(wdir, wdir);
       d3 w = ls ? unit_vector(wdir) : un;
       d3 aa = fabs(w.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
       Onb b;
@@ -1275,14 +1305,22 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       b.w = w;
       double sn, cs;
       sincos2pi(r1, &sn, &cs);
-      double z, rho;
+      // random_to_sphere (object.rs:122-132) / random_cosine_direction (vec3.rs:240-250): one
+      // sqrt serves rho of both, so a wave with both kinds of lanes runs two sqrt, not three
+      double z;
       if (ls) {
-        z = fma(r2, sqrt(1.0 - rad * rad / dist2) - 1.0, 1.0);
-        rho = sqrt(fma(-z, z, 1.0));
+        double cm;
+        if ((int)li == P.sphere_light0) {
+          cm = cos_sl0;
+        } else {
+          const double rad = ldd(L, 3);
+          cm = sqrt(1.0 - rad * rad / dot(wdir, wdir));
+        }
+        z = fma(r2, cm - 1.0, 1.0);
       } else {
         z = sqrt(1.0 - r2);
-        rho = sqrt(r2);
       }
+      const double rho = sqrt(ls ? fma(-z, z, 1.0) : r2);
       d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
       if (lq) {
         local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
@@ -1303,7 +1341,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     double pdf_val = mat_pdf;
     PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
-    if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, C), 0.5 * mat_pdf);  // pdf.rs:116
+    if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, cos_sl0, C), 0.5 * mat_pdf);  // pdf.rs:116
 #endif
     PROF(6);
     beta = beta * (atten * (s_pdf / pdf_val));

@@ -50,7 +50,7 @@
  *   the planar coordinates of object.rs:469-470, a = w.(pq x v) and b = w.(u x pq), are the
  *   same triple products evaluated as a = pq.A, b = pq.B (two dots instead of two crosses and
  *   two dots per test).                                                  object.rs:414-490
- * Light records (LQUAD, 52 words) append d16-19 u.xyz,0 and d20-23 v.xyz,0 for Quad::random
+ * Light records (LQUAD) append d16-19 u.xyz,0 and d20-23 v.xyz,0 for Quad::random
  * (object.rs:503-506). */
 /* World QUAD records (48 words) put an axis-aligned form FIRST, so one 64-byte scalar load
  * covers the header and everything the axis-aligned test reads, and the general payload after it:
@@ -65,7 +65,10 @@
 #define RTL_QUAD_GEN 12
 #define RTL_QUAD_WORDS 48
 #define RTL_QUAD_AXIS(h) (((h) >> 8) & 0x3u)
-#define RTL_LQUAD_WORDS 52
+/* Light QUAD records (64 words) = the general layout, u, v, then the axis-aligned form at
+ * d24-28 (header axis bits as for world quads) for HittablePDF's hit test (object.rs:493). */
+#define RTL_LQUAD_WORDS 64
+#define RTL_LQUAD_AXIS_D 24
 /* SPHERE (20 words): [hdr | moving][skip][mat][next] d0-3 c.xyz,r | d4-7 cvec.xyz,1/r
  *                                                                             object.rs:73-105 */
 #define RTL_SPHERE_MOVING 0x100u
