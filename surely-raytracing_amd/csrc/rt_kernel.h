@@ -332,13 +332,15 @@ __device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, dou
   const double t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
   const double a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
   const double b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
-  bool plane = !(fabs(dk) < 1e-8);
-  bool range = plane && (tmin <= t && t <= tmax);
-  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
+  // bitwise & / |: the predicate is straight-line code; the comparisons are the reference's
+  // (a NaN planar coordinate is accepted, as in object.rs:473)
+  const bool plane = !(fabs(dk) < 1e-8);
+  const bool range = plane & (tmin <= t) & (t <= tmax);
+  const bool hit = range & !((a < 0.0) | (1.0 < a) | (b < 0.0) | (1.0 < b));
   C.inc_if(RT_OP_QUAD_PLANE, plane);
   C.inc_if(RT_OP_QUAD_INTERVAL, range);
   C.inc_if(RT_OP_QUAD_HITS, hit);
-  if (hit) t_out = t;
+  t_out = hit ? t : t_out;
   return hit;
 }
 // A world QUAD record (batch member or single): branch on its axis code (wave-uniform in UNI
@@ -612,15 +614,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       Ptr Q = X + 4;
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
       uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
-#ifdef RT_EXP_PF2
-      uint4 b0, b1, b2, b3;
-      if (!UNI) {
-        ld64(Q, a0, a1, a2, a3);
-        ld64(Q + RTL_QUAD_WORDS, b0, b1, b2, b3);
-      }
-#else
       if (!UNI) ld64(Q, a0, a1, a2, a3);
-#endif
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
         double t;
         bool hq;
@@ -629,21 +623,15 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         } else {
           const AQuad q = {a0.x, hilo(a1.x, a1.y), hilo(a1.z, a1.w), hilo(a2.x, a2.y),
                            hilo(a2.z, a2.w), hilo(a3.x, a3.y)};
-#ifdef RT_EXP_PF2
-          a0 = b0, a1 = b1, a2 = b2, a3 = b3;
-          ld64(Q + 2 * RTL_QUAD_WORDS, b0, b1, b2, b3);  // two quads ahead (padding covers it)
-#else
           ld64(Q + RTL_QUAD_WORDS, a0, a1, a2, a3);  // past the batch: the next node (padded)
-#endif
           hq = aquad_dispatch<COUNT>(q, Q, o, d, r, tmin, closest, t, C);
         }
-        if (hq) {
-          closest = t;
-          hit = true;
-          if (MAIN) {
-            hit_node = (uint32_t)(node + 4 + k * RTL_QUAD_WORDS);
-            hit_frame = frame;
-          }
+        // selects, not a branch: the closest-hit update stays in the straight-line block
+        closest = hq ? t : closest;
+        hit = hit | hq;
+        if (MAIN) {
+          hit_node = hq ? (uint32_t)(node + 4 + k * RTL_QUAD_WORDS) : hit_node;
+          hit_frame = hq ? frame : hit_frame;
         }
       }
       node = h.y;
