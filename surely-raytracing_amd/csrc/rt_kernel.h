@@ -384,18 +384,20 @@ __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double
   double half_b = dot(oc, d);
   double c = dot(oc, oc) - r * r;
   double disc = fma(half_b, half_b, -(a * c));
-  if (disc < 0.0) return false;
-  C.inc(RT_OP_SPHERE_ROOTS);
-  double sqrtd = sqrt(disc);
-  double ra = rcp_nr(a);
-  double root = (-half_b - sqrtd) * ra;
-  if (!(tmin < root && root < tmax)) {
-    root = (sqrtd - half_b) * ra;
-    if (!(tmin < root && root < tmax)) return false;
-  }
-  C.inc(RT_OP_SPHERE_HITS);
-  t_out = root;
-  return true;
+  // straight-line: both roots are formed and the predicate selects (object.rs:157-166); a
+  // negative discriminant gives NaN roots, which the predicate never reads
+  const bool real = !(disc < 0.0);
+  C.inc_if(RT_OP_SPHERE_ROOTS, real);
+  const double sqrtd = sqrt(disc);
+  const double ra = rcp_nr(a);
+  const double near = (-half_b - sqrtd) * ra;
+  const double far = (sqrtd - half_b) * ra;
+  const bool in_near = (tmin < near) & (near < tmax);
+  const bool in_far = (tmin < far) & (far < tmax);
+  const bool hit = real & (in_near | in_far);
+  C.inc_if(RT_OP_SPHERE_HITS, hit);
+  t_out = hit ? (in_near ? near : far) : t_out;
+  return hit;
 }
 
 // Aabb::hit object.rs:340-370 on bounds already in registers (the LANE walker's 64-byte node
@@ -589,7 +591,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
     const Ptr X = N + node;
     uint32_t type = h.x & 0xffu;
     if (type == RTL_QUAD) {
-      double t;
+      double t = closest;
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
       bool hq;
       if (UNI) {
@@ -599,13 +601,11 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
                          hilo(q2.z, q2.w), hilo(q3.x, q3.y)};
         hq = aquad_dispatch<COUNT>(q, X, o, d, r, tmin, closest, t, C);
       }
-      if (hq) {
-        closest = t;
-        hit = true;
-        if (MAIN) {
-          hit_node = node;
-          hit_frame = frame;
-        }
+      closest = hq ? t : closest;
+      hit = hit | hq;
+      if (MAIN) {
+        hit_node = hq ? node : hit_node;
+        hit_frame = hq ? frame : hit_frame;
       }
       node = h.w;
     } else if (type == RTL_QUADS) {
@@ -616,9 +616,9 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
       if (!UNI) ld64(Q, a0, a1, a2, a3);
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
-        double t;
+        double t = closest;
         bool hq;
-        if (UNI) {
+        if (UNI) {  // scalar loads at the point of use (prefetching them raised SGPR pressure)
           hq = world_quad_test<COUNT>(Q, o, d, r, tmin, closest, t, C);
         } else {
           const AQuad q = {a0.x, hilo(a1.x, a1.y), hilo(a1.z, a1.w), hilo(a2.x, a2.y),
@@ -639,14 +639,13 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       if (!UNI) PFW(3, 1);
 #endif
     } else if (type == RTL_SPHERE) {
-      double t;
-      if (sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C)) {
-        closest = t;
-        hit = true;
-        if (MAIN) {
-          hit_node = node;
-          hit_frame = frame;
-        }
+      double t = closest;
+      const bool hs = sphere_test<COUNT>(X, o, d, tm, tmin, closest, t, C);
+      closest = t;
+      hit = hit | hs;
+      if (MAIN) {
+        hit_node = hs ? node : hit_node;
+        hit_frame = hs ? frame : hit_frame;
       }
       node = h.w;
     } else if (type == RTL_BVH) {
@@ -907,7 +906,7 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
     double pv = 0.0;
     if (type == RTL_QUAD) {
       C.inc(RT_OP_LIGHT_PDF_QUAD);
-      double t;
+      double t = 0.0;
       bool hq;
       const uint32_t axis = RTL_QUAD_AXIS(L[0]);
       if (axis) {  // axis-aligned form at d24 (rt_layout.h): the world quads' bit-identical test
@@ -931,7 +930,7 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
       }
     } else if (type == RTL_SPHERE) {
       C.inc(RT_OP_LIGHT_PDF_SPHERE);
-      double t;
+      double t = 0.0;
       if (sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C)) {
         double cos_max;
         if ((int)i == P.sphere_light0) {
