@@ -107,6 +107,17 @@ __device__ __forceinline__ double rsq_nr(double x) {
   y = y * fma(-h * y, y, 1.5);
   return y * fma(-h * y, y, 1.5);
 }
+// Radiance weights only (PDF values, scattering PDF, the throughput factor): 1/b by rcp + two
+// Newton steps. Weights never steer a path (directions, hits and draws do), so their last-ulp
+// rounding is free to differ from an IEEE quotient (the CPU oracle, which follows the recursive
+// (atten*s_pdf*L)/pdf form, already differs there); 1/0 = inf and 1/inf = 0 are kept, so the
+// reference's inf/NaN weights (render.rs:289-290) stay inf/NaN.
+__device__ __forceinline__ double rcp_w(double b) {
+  const double r0 = __builtin_amdgcn_rcp(b);
+  double r = fma(fma(-b, r0, 1.0), r0, r0);
+  r = fma(fma(-b, r, 1.0), r, r);
+  return (r0 == 0.0 || __builtin_isinf(r0)) ? r0 : r;
+}
 __device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
   return v * rsq_nr(dot(v, v));
 }
@@ -922,27 +933,28 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
       } else {
         hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
       }
-      if (hq) {
-        double len2 = dot(dir, dir);
-        double dist2 = (t * t) * len2;
-        double cosine = fabs(dot(dir, ld3(L, 0)) / sqrt(len2));
-        pv = dist2 / (cosine * ldd(L, 7));
+      {  // straight-line; weights: rsq/rcp Newton instead of the IEEE sqrt and divisions
+        const double len2 = dot(dir, dir);
+        const double dist2 = (t * t) * len2;
+        const double cosine = fabs(dot(dir, ld3(L, 0))) * rsq_nr(len2);
+        const double q = dist2 * rcp_w(cosine * ldd(L, 7));
+        pv = hq ? q : 0.0;
       }
     } else if (type == RTL_SPHERE) {
       C.inc(RT_OP_LIGHT_PDF_SPHERE);
       double t = 0.0;
-      if (sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C)) {
-        double cos_max;
-        if ((int)i == P.sphere_light0) {
-          cos_max = cos_sl0;
-        } else {
-          d3 cmo = ld3(L, 0) - origin;
-          double r = ldd(L, 3);
-          cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
-        }
-        double solid = 2.0 * kPi * (1.0 - cos_max);
-        pv = 1.0 / solid;
+      const bool hs = sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C);
+      double cos_max = 0.0;
+      if ((int)i == P.sphere_light0) {  // uniform: the shared value (straight-line)
+        cos_max = cos_sl0;
+      } else if (hs) {
+        d3 cmo = ld3(L, 0) - origin;
+        double r = ldd(L, 3);
+        cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
       }
+      const double solid = 2.0 * kPi * (1.0 - cos_max);
+      const double q = rcp_w(solid);
+      pv = hs ? q : 0.0;
     }
     sum = i == 0 ? pv : sum + pv;
   }
@@ -1223,115 +1235,128 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       --depth;
       continue;
     }
-    if (kind == RT_MAT_DIELECTRIC) {  // material.rs:166-191
-      C.inc(RT_OP_DIELECTRIC);
-      double ratio = front ? ldd(M, 4) : ldd(M, 3);  // 1/ir : ir
-      d3 ud = unit_vector(rd);
-      double cos_t = fmin(dot(-ud, normal), 1.0);
-      double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
-      bool refl = ratio * sin_t > 1.0;
-      if (!refl) {
-        double r0 = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
-        double xx = 1.0 - cos_t;
-        double x2 = xx * xx;
-        refl = fma(1.0 - r0, x2 * x2 * xx, r0) > rnd(g);
-      }
-      rd = refl ? reflect(ud, normal) : refract(ud, normal, ratio);
-      beta = beta * ld3(M, 0);
-      ro = p;
-      --depth;
-      continue;
-    }
-    // Lambertian / Isotropic: mixture-PDF branch render.rs:278-292
+    // Dielectric (material.rs:166-191), Lambertian and Isotropic (the mixture-PDF branch,
+    // render.rs:278-292) run as ONE block: a wave holding both kinds of lanes shares the unit
+    // vector, the first sqrt, the first uniform draw and the throughput update instead of
+    // running two exclusive branches. Per lane the arithmetic and the draw order are exactly
+    // those of the separate branches.
     PROF(4);
+    const bool diel = kind == RT_MAT_DIELECTRIC;
     const bool iso = kind == RT_MAT_ISOTROPIC;
-    C.inc(iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN);
-    d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
-    // Draw order as the reference: mixture coin (pdf.rs:120-126), then light index
-    // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
-    bool light_branch = false;
-    if (have_lights) light_branch = rnd(g) < 0.5;
-    uint32_t ltype = 0, li = 0;
-    gptr L = T.lights;
-    // cos_theta_max of the first sphere light at p (object.rs:196, 205-207; -1 = none)
-    double cos_sl0 = 0.0;
+    C.inc(diel ? RT_OP_DIELECTRIC : (iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN));
+    // unit(r_in.direction) (material.rs:170) or CosinePDF's w = unit(normal) (pdf.rs:58-62)
+    const d3 uu = unit_vector(diel ? rd : normal);
+    const double ratio = front ? ldd(M, 4) : ldd(M, 3);  // dielectric: 1/ir : ir
+    const double cos_t = fmin(dot(-uu, normal), 1.0);     // material.rs:172
+    // first sqrt: the dielectric's sin(theta) (material.rs:173) or cos_theta_max of the first
+    // sphere light at p (object.rs:196, 205-207), shared by Sphere::random and pdf_value
+    double sq_in = fma(-cos_t, cos_t, 1.0);
     if (P.sphere_light0 >= 0) {
       const gptr S0 = T.lights + T.loffs[P.sphere_light0];
       const d3 cmo = ld3(S0, 0) - p;
       const double r0 = ldd(S0, 3);
-      cos_sl0 = sqrt(1.0 - r0 * r0 / dot(cmo, cmo));
+      const double arg = 1.0 - r0 * r0 / dot(cmo, cmo);
+      sq_in = diel ? sq_in : arg;
     }
-    if (light_branch) {
-      C.inc(RT_OP_LIGHT_GEN);
-      li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
-      L = T.lights + T.loffs[li];
-      ltype = L[0] & 0xffu;
-    } else {
-      C.inc(RT_OP_COSINE_GEN);
-    }
-    d3 dir;
-    const d3 un = unit_vector(normal);  // CosinePDF's w (pdf.rs:58-62, onb.rs:33)
-    if (iso && !light_branch) {
-      dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
-    } else if (light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
-      dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
-    } else {
-      // Quad::random (object.rs:503-506), Sphere::random / random_to_sphere (204-212, 122-132)
-      // and CosinePDF::generate (pdf.rs:75-77, vec3.rs:240-250) share one straight-line block:
-      // one ONB, one sincos, selects instead of divergent branches.
-      const double r1 = rnd(g), r2 = rnd(g);
-      const bool lq = light_branch && ltype == RTL_QUAD;
-      const bool ls = light_branch && ltype == RTL_SPHERE;
-      d3 c = ls ? ld3(L, 0) : p;
-      d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
-      d3 w = ls ? unit_vector(wdir) : un;
-      d3 aa = fabs(w.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
-      Onb b;
-      b.v = unit_vector(cross(w, aa));
-      b.u = cross(w, b.v);
-      b.w = w;
-      double sn, cs;
-      sincos2pi(r1, &sn, &cs);
-      // random_to_sphere (object.rs:122-132) / random_cosine_direction (vec3.rs:240-250): one
-      // sqrt serves rho of both, so a wave with both kinds of lanes runs two sqrt, not three
-      double z;
-      if (ls) {
-        double cm;
-        if ((int)li == P.sphere_light0) {
-          cm = cos_sl0;
-        } else {
-          const double rad = ldd(L, 3);
-          cm = sqrt(1.0 - rad * rad / dot(wdir, wdir));
-        }
-        z = fma(r2, cm - 1.0, 1.0);
+    const double sq = sqrt(sq_in);
+    const double cos_sl0 = sq;
+    const bool tir = diel && ratio * sq > 1.0;  // cannot_refract (material.rs:175)
+    // first uniform: the Schlick test, drawn only when not TIR (material.rs:180), or the
+    // mixture coin (pdf.rs:120-126)
+    double u0 = 0.0;
+    if (diel ? !tir : have_lights) u0 = rnd(g);
+    const double r0s = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
+    const double xx = 1.0 - cos_t;
+    const double x2 = xx * xx;
+    const bool refl = tir || fma(1.0 - r0s, x2 * x2 * xx, r0s) > u0;
+    const bool light_branch = !diel && have_lights && u0 < 0.5;
+    d3 dir = mk(0., 0., 0.), factor = mk(0., 0., 0.);
+    double cos_sl = cos_sl0;
+    if (!diel) {
+      d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
+      // Draw order as the reference: mixture coin (above), then light index
+      // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
+      uint32_t ltype = 0, li = 0;
+      gptr L = T.lights;
+      if (light_branch) {
+        C.inc(RT_OP_LIGHT_GEN);
+        li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
+        L = T.lights + T.loffs[li];
+        ltype = L[0] & 0xffu;
       } else {
-        z = sqrt(1.0 - r2);
+        C.inc(RT_OP_COSINE_GEN);
       }
-      const double rho = sqrt(ls ? fma(-z, z, 1.0) : r2);
-      d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
-      if (lq) {
-        local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
+      const d3 un = uu;
+      if (iso && !light_branch) {
+        dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
+      } else if (light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
+        dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
+      } else {
+        // Quad::random (object.rs:503-506), Sphere::random / random_to_sphere (204-212, 122-132)
+        // and CosinePDF::generate (pdf.rs:75-77, vec3.rs:240-250) share one straight-line block:
+        // one ONB, one sincos, selects instead of divergent branches.
+        const double r1 = rnd(g), r2 = rnd(g);
+        const bool lq = light_branch && ltype == RTL_QUAD;
+        const bool ls = light_branch && ltype == RTL_SPHERE;
+        d3 c = ls ? ld3(L, 0) : p;
+        d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
+        d3 w = ls ? unit_vector(wdir) : un;
+        d3 aa = fabs(w.x) > 0.9 ? mk(0., 1., 0.) : mk(1., 0., 0.);
+        Onb b;
+        b.v = unit_vector(cross(w, aa));
+        b.u = cross(w, b.v);
+        b.w = w;
+        double sn, cs;
+        sincos2pi(r1, &sn, &cs);
+        // random_to_sphere (object.rs:122-132) / random_cosine_direction (vec3.rs:240-250): one
+        // sqrt serves rho of both, so a wave with both kinds of lanes runs two sqrt, not three
+        double z;
+        if (ls) {
+          double cm;
+          if ((int)li == P.sphere_light0) {
+            cm = cos_sl0;
+          } else {
+            const double rad = ldd(L, 3);
+            cm = sqrt(1.0 - rad * rad / dot(wdir, wdir));
+          }
+          z = fma(r2, cm - 1.0, 1.0);
+        } else {
+          z = sqrt(1.0 - r2);
+        }
+        const double rho = sqrt(ls ? fma(-z, z, 1.0) : r2);
+        d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
+        if (lq) {
+          local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
+        }
+        dir = local;
       }
-      dir = local;
-    }
-    double mat_pdf, s_pdf;
-    if (iso) {
-      mat_pdf = 1.0 / (4.0 * kPi);                   // SpherePDF::value pdf.rs:47-49
-      s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
-    } else {
-      d3 udir = unit_vector(dir);
-      double cv = dot(udir, un) / kPi;               // CosinePDF::value pdf.rs:69-73
-      mat_pdf = cv > 0.0 ? cv : 0.0;
-      double cs = dot(normal, udir);                 // Lambertian::scattering_pdf 100-108
-      s_pdf = cs < 0.0 ? 0.0 : cs / kPi;
-    }
-    double pdf_val = mat_pdf;
-    PROF(5);
+      double mat_pdf, s_pdf;
+      if (iso) {
+        mat_pdf = 1.0 / (4.0 * kPi);                   // SpherePDF::value pdf.rs:47-49
+        s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
+      } else {
+        d3 udir = unit_vector(dir);
+        double cv = dot(udir, un) * (1.0 / kPi);       // CosinePDF::value pdf.rs:69-73
+        mat_pdf = cv > 0.0 ? cv : 0.0;
+        double csn = dot(normal, udir);                // Lambertian::scattering_pdf 100-108
+        s_pdf = csn < 0.0 ? 0.0 : csn * (1.0 / kPi);
+      }
+      double pdf_val = mat_pdf;
+      PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
-    if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, cos_sl0, C), 0.5 * mat_pdf);  // pdf.rs:116
+      if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, cos_sl, C), 0.5 * mat_pdf);  // pdf.rs:116
 #endif
-    PROF(6);
-    beta = beta * (atten * (s_pdf / pdf_val));
+      PROF(6);
+      factor = atten * (s_pdf * rcp_w(pdf_val));
+    }
+    if (diel) {
+      // reflect (vec3.rs:219-221) or refract (vec3.rs:223-229; its cos_theta is cos_t)
+      const d3 perp = ratio * vfma(cos_t, normal, uu);
+      const d3 refr = vfma(-sqrt(fabs(1.0 - dot(perp, perp))), normal, perp);
+      dir = refl ? reflect(uu, normal) : refr;
+      factor = ld3(M, 0);  // attenuation = tint
+    }
+    beta = beta * factor;
     ro = p;
     rd = dir;
     --depth;

@@ -2,6 +2,10 @@
 import sys
 sys.path.insert(0, "surely-raytracing_amd")
 import surely_rt as rt  # noqa: E402
+import os  # noqa: E402
+
+if os.environ.get("RT_LIB"):  # profiling a library variant (tools only; the product loads build/)
+    rt._dev = rt.load_device_lib(os.environ["RT_LIB"])
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell_box"
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 800
