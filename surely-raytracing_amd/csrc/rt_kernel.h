@@ -626,6 +626,8 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
       uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
       if (!UNI) ld64(Q, a0, a1, a2, a3);
+      // the batch's winner is tracked as an index: one select per quad instead of three
+      uint32_t hk = ~0u;
       for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
         double t = closest;
         bool hq;
@@ -639,11 +641,13 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         }
         // selects, not a branch: the closest-hit update stays in the straight-line block
         closest = hq ? t : closest;
-        hit = hit | hq;
-        if (MAIN) {
-          hit_node = hq ? (uint32_t)(node + 4 + k * RTL_QUAD_WORDS) : hit_node;
-          hit_frame = hq ? frame : hit_frame;
-        }
+        hk = hq ? k : hk;
+      }
+      const bool hb = hk != ~0u;
+      hit = hit | hb;
+      if (MAIN) {
+        hit_node = hb ? (uint32_t)(node + 4 + hk * RTL_QUAD_WORDS) : hit_node;
+        hit_frame = hb ? frame : hit_frame;
       }
       node = h.y;
 #ifdef RT_PROF
