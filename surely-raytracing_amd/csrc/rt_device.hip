@@ -38,10 +38,10 @@ using namespace rtk;
 namespace {
 
 // Ahead-of-time kernels: the interpreter traversal, one per feature combination.
-template <bool COUNT, bool VOL, bool TEX, bool BVH>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED>
 __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(
     TraceParams P) {
-  trace_body<COUNT, VOL, TEX, BVH, TravInterp>(P);
+  trace_body<COUNT, VOL, TEX, BVH, STAGED, TravInterp>(P);
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
@@ -125,8 +125,8 @@ struct rt_scene {
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
-  int resident_blocks[16] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
-  size_t resident_lds[16] = {};  // ... at this dynamic LDS size
+  int resident_blocks[32] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
+  size_t resident_lds[32] = {};  // ... at this dynamic LDS size
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -384,19 +384,27 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
   const bool bvh = sc->hdr.has_bvh != 0;
   typedef void (*kern_t)(TraceParams);
-  // [count][vol][tex][bvh]
+  // [count][vol][tex][bvh]; a scene without a BVH whose tables are staged in LDS runs the
+  // STAGED variant (LDS-typed table reads), BVH kernels read the tables from global memory
   static const kern_t table[16] = {
-      rt_trace<false, false, false, false>, rt_trace<false, false, false, true>,
-      rt_trace<false, false, true, false>,  rt_trace<false, false, true, true>,
-      rt_trace<false, true, false, false>,  rt_trace<false, true, false, true>,
-      rt_trace<false, true, true, false>,   rt_trace<false, true, true, true>,
-      rt_trace<true, false, false, false>,  rt_trace<true, false, false, true>,
-      rt_trace<true, false, true, false>,   rt_trace<true, false, true, true>,
-      rt_trace<true, true, false, false>,   rt_trace<true, true, false, true>,
-      rt_trace<true, true, true, false>,    rt_trace<true, true, true, true>};
+      rt_trace<false, false, false, false, false>, rt_trace<false, false, false, true, false>,
+      rt_trace<false, false, true, false, false>,  rt_trace<false, false, true, true, false>,
+      rt_trace<false, true, false, false, false>,  rt_trace<false, true, false, true, false>,
+      rt_trace<false, true, true, false, false>,   rt_trace<false, true, true, true, false>,
+      rt_trace<true, false, false, false, false>,  rt_trace<true, false, false, true, false>,
+      rt_trace<true, false, true, false, false>,   rt_trace<true, false, true, true, false>,
+      rt_trace<true, true, false, false, false>,   rt_trace<true, true, false, true, false>,
+      rt_trace<true, true, true, false, false>,    rt_trace<true, true, true, true, false>};
+  // [count][vol][tex], no BVH, staged
+  static const kern_t table_staged[8] = {
+      rt_trace<false, false, false, false, true>, rt_trace<false, false, true, false, true>,
+      rt_trace<false, true, false, false, true>,  rt_trace<false, true, true, false, true>,
+      rt_trace<true, false, false, false, true>,  rt_trace<true, false, true, false, true>,
+      rt_trace<true, true, false, false, true>,   rt_trace<true, true, true, false, true>};
+  const bool staged = !bvh && P.stage_scene;
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
-                   (bvh ? 1 : 0);
-  kern_t kern = table[kidx];
+                   (bvh ? 1 : 0) + (staged ? 16 : 0);
+  kern_t kern = staged ? table_staged[kidx / 2 - 8] : table[kidx];
   const int block = bvh ? kBlockBvh : kBlock;
   if (lds_bytes > (64u << 10))
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,

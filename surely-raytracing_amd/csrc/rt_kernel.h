@@ -171,10 +171,11 @@ constexpr uint32_t kPerlinLds = 4;
 constexpr size_t kStageScene = 24u << 10;
 extern __shared__ __attribute__((aligned(16))) uint8_t rt_lds[];
 
-// Table pointers for per-lane (divergent) reads: the workgroup's LDS copy of a small scene, or
-// the global tables. Generic pointers: the same code reads either.
-struct Tabs {
-  const uint32_t *nodes, *mats, *texs, *lights, *loffs;
+// Table pointers for per-lane (divergent) reads: TP = lptr for the workgroup's LDS copy of a
+// small scene (ds_read, 32-bit addresses: one SGPR per table), gptr for the global tables.
+template <class TP>
+struct TabsT {
+  TP nodes, mats, texs, lights, loffs;
   const uint8_t* perlin;  // LDS: the staged Perlin tables
 };
 
@@ -235,6 +236,13 @@ __device__ __forceinline__ d3 karr3(const __attribute__((address_space(4))) doub
 typedef const uint32_t* gptr;
 typedef const __attribute__((address_space(4))) uint32_t* kptr;
 typedef const __attribute__((address_space(4))) double* kdptr;
+//  lptr: the LDS copy of a staged small scene (per-lane reads as ds_read)
+typedef const __attribute__((address_space(3))) uint32_t* lptr;
+typedef const __attribute__((address_space(3))) double* ldptr;
+typedef double v2d __attribute__((ext_vector_type(2)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(3))) v2d* ld2ptr;
+typedef const __attribute__((address_space(3))) v4u* lu4ptr;
 
 __device__ __forceinline__ d3 ld3(gptr X, int k) {  // f64 triple at payload double index k
   const double* d = reinterpret_cast<const double*>(X + 4) + k;
@@ -254,6 +262,20 @@ __device__ __forceinline__ double ldd(gptr X, int k) {
 }
 __device__ __forceinline__ double ldd(kptr X, int k) { return reinterpret_cast<kdptr>(X + 4)[k]; }
 __device__ __forceinline__ uint4 ld4u(gptr p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ d3 ld3(lptr X, int k) {
+  ldptr d = reinterpret_cast<ldptr>(X + 4) + k;
+  if ((k & 1) == 0) {
+    const v2d a = *reinterpret_cast<ld2ptr>(d);
+    return mk(a.x, a.y, d[2]);
+  }
+  const v2d b = *reinterpret_cast<ld2ptr>(d + 1);
+  return mk(d[0], b.x, b.y);
+}
+__device__ __forceinline__ double ldd(lptr X, int k) { return reinterpret_cast<ldptr>(X + 4)[k]; }
+__device__ __forceinline__ uint4 ld4u(lptr p) {
+  const v4u v = *reinterpret_cast<lu4ptr>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint4 ld4u(kptr p) { return make_uint4(p[0], p[1], p[2], p[3]); }
 // first 64 bytes of a node record: four independent 16-byte loads, one memory round trip
 template <class Ptr>
@@ -463,7 +485,8 @@ __device__ __forceinline__ void xform_in(Ptr X, d3& o, d3& d) {
   }
 }
 // Hit record back to the parent space (transform.rs:65, 114-130).
-__device__ __forceinline__ void xform_out(gptr X, d3& p, d3& n) {
+template <class Ptr>
+__device__ __forceinline__ void xform_out(Ptr X, d3& p, d3& n) {
   if ((X[0] & 0xffu) == RTL_TRANSLATE) {
     p = p + ld3(X, 2);
   } else {
@@ -829,12 +852,12 @@ __device__ __noinline__ double perlin_turb_global(const uint8_t* __restrict__ T,
   return perlin_turb(T, p);
 }
 
-template <bool COUNT, bool TEX>
-__device__ d3 tex_value(const TraceParams& P, const Tabs& T, uint32_t id, double u, double v,
+template <bool COUNT, bool TEX, class TT>
+__device__ d3 tex_value(const TraceParams& P, const TT& T, uint32_t id, double u, double v,
                         d3 p, Ctr<COUNT>& C) {
   if (!TEX) return ld3(T.texs + (size_t)id * RTL_TEX_WORDS, 0);
   for (int guard = 0; guard < 65; ++guard) {
-    const uint32_t* t = T.texs + (size_t)id * RTL_TEX_WORDS;
+    const auto t = T.texs + (size_t)id * RTL_TEX_WORDS;
     uint4 h = ld4u(t);
     if (h.x == RT_TEX_SOLID) return ld3(t, 0);
     if (h.x == RT_TEX_CHECKER) {  // texture.rs:71-81
@@ -989,8 +1012,11 @@ struct TravInterp {
 
 // The path kernel body; instantiated by rt_device.hip (interpreter) and by scene-specialised
 // JIT kernels. Its __global__ wrapper passes TraceParams as the only kernel argument (kparams()).
-template <bool COUNT, bool VOL, bool TEX, bool BVH, class Trav>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, class Trav>
 __device__ __forceinline__ void trace_body(const TraceParams& P) {
+  // STAGED: the small-table prefix is in LDS (P.stage_scene) and per-lane table reads are
+  // ds_reads through 32-bit LDS pointers; otherwise they read the global tables.
+  typedef typename cond<STAGED, lptr, gptr>::type TP;
   __shared__ unsigned int sh_ops[COUNT ? RT_OP_COUNT : 1];
   if (COUNT) {
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
@@ -1010,14 +1036,23 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     }
     __syncthreads();
   }
-  Tabs T;
-  {
-    const uint8_t* b = P.stage_scene ? (const uint8_t*)rt_lds : (const uint8_t*)P.nodes;
-    T.nodes = reinterpret_cast<const uint32_t*>(b);
-    T.mats = reinterpret_cast<const uint32_t*>(b + P.o_mats);
-    T.texs = reinterpret_cast<const uint32_t*>(b + P.o_texs);
-    T.lights = reinterpret_cast<const uint32_t*>(b + P.o_lights);
-    T.loffs = reinterpret_cast<const uint32_t*>(b + P.o_loffs);
+  TabsT<TP> T;
+  if constexpr (STAGED) {
+    typedef const __attribute__((address_space(3))) uint8_t* lbptr;
+    const lbptr b = (lbptr)rt_lds;
+    T.nodes = reinterpret_cast<lptr>(b);
+    T.mats = reinterpret_cast<lptr>(b + P.o_mats);
+    T.texs = reinterpret_cast<lptr>(b + P.o_texs);
+    T.lights = reinterpret_cast<lptr>(b + P.o_lights);
+    T.loffs = reinterpret_cast<lptr>(b + P.o_loffs);
+    T.perlin = rt_lds + P.o_perl;
+  } else {
+    const uint8_t* b = (const uint8_t*)P.nodes;
+    T.nodes = reinterpret_cast<gptr>(b);
+    T.mats = reinterpret_cast<gptr>(b + P.o_mats);
+    T.texs = reinterpret_cast<gptr>(b + P.o_texs);
+    T.lights = reinterpret_cast<gptr>(b + P.o_lights);
+    T.loffs = reinterpret_cast<gptr>(b + P.o_loffs);
     T.perlin = rt_lds + (P.stage_scene ? P.o_perl : 0u);
   }
   Ctr<COUNT> C;
@@ -1180,7 +1215,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
     PROF(2);
-    const uint32_t* X = T.nodes + hn;
+    const TP X = T.nodes + hn;
     uint32_t type = X[0] & 0xffu;
     d3 o, d;
     frame_ray(T.nodes, hf, ro, rd, o, d);
@@ -1188,11 +1223,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     d3 normal;
     bool front = true;
     double u = 0., v = 0.;
-    const uint32_t* M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
+    const TP M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
     uint4 mh = ld4u(M);
     const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
     if (type == RTL_QUAD) {
-      const gptr XG = X + RTL_QUAD_GEN;
+      const TP XG = X + RTL_QUAD_GEN;
       d3 n = ld3(XG, 0);
       front = dot(d, n) < 0.0;  // set_face_normal hittable.rs:22-37
       normal = front ? n : -n;
@@ -1256,7 +1291,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // sphere light at p (object.rs:196, 205-207), shared by Sphere::random and pdf_value
     double sq_in = fma(-cos_t, cos_t, 1.0);
     if (P.sphere_light0 >= 0) {
-      const gptr S0 = T.lights + T.loffs[P.sphere_light0];
+      const TP S0 = T.lights + T.loffs[P.sphere_light0];
       const d3 cmo = ld3(S0, 0) - p;
       const double r0 = ldd(S0, 3);
       const double arg = 1.0 - r0 * r0 / dot(cmo, cmo);
@@ -1281,7 +1316,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       // Draw order as the reference: mixture coin (above), then light index
       // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
       uint32_t ltype = 0, li = 0;
-      gptr L = T.lights;
+      TP L = T.lights;
       if (light_branch) {
         C.inc(RT_OP_LIGHT_GEN);
         li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
