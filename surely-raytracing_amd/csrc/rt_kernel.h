@@ -326,13 +326,14 @@ __device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double
   d3 pq = vfma(t, d, o) - ld3(q, 4);
   double a = dot(pq, ld3(q, 8));
   double b = dot(pq, ld3(q, 12));
-  bool plane = !(fabs(denom) < 1e-8);
-  bool range = plane && (tmin <= t && t <= tmax);
-  bool hit = range && !(a < 0.0 || 1.0 < a || b < 0.0 || 1.0 < b);
+  const bool plane = !(fabs(denom) < 1e-8);
+  const bool range = plane & (tmin <= t) & (t <= tmax);
+  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);  // as in aquad_test
+  const bool hit = range & !(lo < 0.0) & !(1.0 < hi);
   C.inc_if(RT_OP_QUAD_PLANE, plane);
   C.inc_if(RT_OP_QUAD_INTERVAL, range);
   C.inc_if(RT_OP_QUAD_HITS, hit);
-  if (hit) t_out = t;
+  t_out = hit ? t : t_out;
   return hit;
 }
 
@@ -365,11 +366,13 @@ __device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, dou
   const double t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
   const double a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
   const double b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
-  // bitwise & / |: the predicate is straight-line code; the comparisons are the reference's
-  // (a NaN planar coordinate is accepted, as in object.rs:473)
+  // straight-line predicate. a, b in [0, 1] as min/max (IEEE minNum/maxNum): min(a, b) < 0 or
+  // 1 < max(a, b) exactly when the reference rejects (object.rs:473), NaN included (a NaN
+  // coordinate drops out of min/max, and the reference's comparisons accept it too)
   const bool plane = !(fabs(dk) < 1e-8);
   const bool range = plane & (tmin <= t) & (t <= tmax);
-  const bool hit = range & !((a < 0.0) | (1.0 < a) | (b < 0.0) | (1.0 < b));
+  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+  const bool hit = range & !(lo < 0.0) & !(1.0 < hi);
   C.inc_if(RT_OP_QUAD_PLANE, plane);
   C.inc_if(RT_OP_QUAD_INTERVAL, range);
   C.inc_if(RT_OP_QUAD_HITS, hit);
@@ -635,7 +638,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
                          hilo(q2.z, q2.w), hilo(q3.x, q3.y)};
         hq = aquad_dispatch<COUNT>(q, X, o, d, r, tmin, closest, t, C);
       }
-      closest = hq ? t : closest;
+      closest = t;  // t_out is only written on a hit (t started as closest)
       hit = hit | hq;
       if (MAIN) {
         hit_node = hq ? node : hit_node;
@@ -663,7 +666,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
           hq = aquad_dispatch<COUNT>(q, Q, o, d, r, tmin, closest, t, C);
         }
         // selects, not a branch: the closest-hit update stays in the straight-line block
-        closest = hq ? t : closest;
+        closest = t;  // t_out is only written on a hit (t started as closest)
         hk = hq ? k : hk;
       }
       const bool hb = hk != ~0u;

@@ -59,6 +59,48 @@ __global__ void __launch_bounds__(256) rcp64(double* out, int iters) {
   if (s == 12345.678) out[0] = s;
 }
 
+// 32-bit integer multiply (v_mul_lo_u32) and xor throughput, 8 independent chains
+template <int OP>
+__global__ void __launch_bounds__(256) int32op(unsigned* out, unsigned a, int iters) {
+  unsigned x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x * 7u + k;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (OP == 0) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[k]) : "v"(a));
+        else if (OP == 1) x[k] = (x[k] ^ a) + k;
+        else asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(x[k]) : "v"(a));
+      }
+  }
+  unsigned s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == 0xdeadbeef) out[0] = s;
+}
+// f64 compare + select (v_cmp_f64 / v_cndmask_b32 x2) throughput, 8 chains
+__global__ void __launch_bounds__(256) cmpsel64(double* out, double a, int iters) {
+  double x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = threadIdx.x * 1e-3 + k;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        double y = x[k];
+        asm volatile("" : "+v"(y));
+        x[k] = x[k] < a ? y : a;
+      }
+  }
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += x[k];
+  if (s == 12345.678) out[0] = s;
+}
+
 // dependent scalar loads: a wave-uniform pointer chase through a small table
 __global__ void __launch_bounds__(256) schase(const unsigned* __restrict__ tab, unsigned* out,
                                               int iters) {
@@ -124,6 +166,10 @@ int main() {
     report("rcp64 dep (1 chain)", time_it([](int g) { rcp64<1><<<g, 256>>>(g_d, ITERS); }, grid), ITERS * 8.0);
     report("rcp64 8 chains", time_it([](int g) { rcp64<8><<<g, 256>>>(g_d, ITERS); }, grid), ITERS * 64.0);
     report("s_load chase", time_it([](int g) { schase<<<g, 256>>>(g_tab, g_u, ITERS); }, grid), ITERS * 1.0);
+    report("mul_lo_u32 8 chains", time_it([](int g) { int32op<0><<<g, 256>>>(g_u, 2654435761u, ITERS); }, grid), ITERS * 64.0);
+    report("v_xad_u32 8 chains", time_it([](int g) { int32op<1><<<g, 256>>>(g_u, 2654435761u, ITERS); }, grid), ITERS * 64.0);
+    report("mul_u32_u24 8 chains", time_it([](int g) { int32op<2><<<g, 256>>>(g_u, 2654435761u, ITERS); }, grid), ITERS * 64.0);
+    report("cmp f64+2 cndmask 8ch", time_it([](int g) { cmpsel64<<<g, 256>>>(g_d, 0.5, ITERS); }, grid), ITERS * 64.0);
   }
   return 0;
 }
