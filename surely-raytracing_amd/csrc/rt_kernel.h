@@ -118,6 +118,22 @@ __device__ __forceinline__ double rcp_w(double b) {
   r = fma(fma(-b, r, 1.0), r, r);
   return (r0 == 0.0 || __builtin_isinf(r0)) ? r0 : r;
 }
+// sqrt from v_rsq_f64 plus one Goldschmidt/Newton refinement of (s, h) = (sqrt x, 1/(2 sqrt x))
+// and a final residual correction: within an ulp of the IEEE root (like rsq_nr / div_nr, the
+// device's geometry rounding) at about half the library sequence. +-0 and +inf
+// return themselves, negative and NaN inputs give NaN, as IEEE sqrt does. Inputs here are
+// never subnormal (uniform draws are multiples of 2^-32; squared unit-scale cosines).
+__device__ __forceinline__ double sqrt_nr(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double s = x * y;
+  double h = 0.5 * y;
+  const double r = fma(-s, h, 0.5);
+  s = fma(s, r, s);
+  h = fma(h, r, h);
+  const double e = fma(-s, s, x);
+  s = fma(e, h, s);
+  return __builtin_amdgcn_class(x, 0x260) ? x : s;  // +-0, +inf
+}
 __device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
   return v * rsq_nr(dot(v, v));
 }
@@ -127,7 +143,7 @@ __device__ __forceinline__ d3 reflect(d3 v, d3 n) {  // vec3.rs:219-221
 __device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-229
   double c = fmin(dot(-uv, n), 1.0);
   d3 perp = e * vfma(c, n, uv);
-  return vfma(-sqrt(fabs(1.0 - dot(perp, perp))), n, perp);
+  return vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), n, perp);
 }
 
 // sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (vec3.rs:244, object.rs:127: phi = 2*pi*r1).
@@ -424,7 +440,7 @@ __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double
   // negative discriminant gives NaN roots, which the predicate never reads
   const bool real = !(disc < 0.0);
   C.inc_if(RT_OP_SPHERE_ROOTS, real);
-  const double sqrtd = sqrt(disc);
+  const double sqrtd = sqrt_nr(disc);
   const double ra = rcp_nr(a);
   const double near = (-half_b - sqrtd) * ra;
   const double far = (sqrtd - half_b) * ra;
@@ -920,8 +936,8 @@ __device__ __forceinline__ d3 random_cosine_direction(Rng& g) {  // vec3.rs:240-
   double r2 = rnd(g);
   double s, c;
   sincos2pi(r1, &s, &c);
-  double sq = sqrt(r2);
-  return mk(c * sq, s * sq, sqrt(1.0 - r2));
+  double sq = sqrt_nr(r2);
+  return mk(c * sq, s * sq, sqrt_nr(1.0 - r2));
 }
 __device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 231-238
   for (;;) {
@@ -980,7 +996,7 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
       } else if (hs) {
         d3 cmo = ld3(L, 0) - origin;
         double r = ldd(L, 3);
-        cos_max = sqrt(1.0 - r * r / dot(cmo, cmo));
+        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));
       }
       const double solid = 2.0 * kPi * (1.0 - cos_max);
       const double q = rcp_w(solid);
@@ -1300,7 +1316,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const double arg = 1.0 - r0 * r0 / dot(cmo, cmo);
       sq_in = diel ? sq_in : arg;
     }
-    const double sq = sqrt(sq_in);
+    const double sq = sqrt_nr(sq_in);
     const double cos_sl0 = sq;
     const bool tir = diel && ratio * sq > 1.0;  // cannot_refract (material.rs:175)
     // first uniform: the Schlick test, drawn only when not TIR (material.rs:180), or the
@@ -1359,13 +1375,13 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
             cm = cos_sl0;
           } else {
             const double rad = ldd(L, 3);
-            cm = sqrt(1.0 - rad * rad / dot(wdir, wdir));
+            cm = sqrt_nr(1.0 - rad * rad / dot(wdir, wdir));
           }
           z = fma(r2, cm - 1.0, 1.0);
         } else {
-          z = sqrt(1.0 - r2);
+          z = sqrt_nr(1.0 - r2);
         }
-        const double rho = sqrt(ls ? fma(-z, z, 1.0) : r2);
+        const double rho = sqrt_nr(ls ? fma(-z, z, 1.0) : r2);
         d3 local = onb_local(b, mk(cs * rho, sn * rho, z));
         if (lq) {
           local = vfma(r2, ld3(L, 20), vfma(r1, ld3(L, 16), ld3(L, 4))) - p;
@@ -1394,7 +1410,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (diel) {
       // reflect (vec3.rs:219-221) or refract (vec3.rs:223-229; its cos_theta is cos_t)
       const d3 perp = ratio * vfma(cos_t, normal, uu);
-      const d3 refr = vfma(-sqrt(fabs(1.0 - dot(perp, perp))), normal, perp);
+      const d3 refr = vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), normal, perp);
       dir = refl ? reflect(uu, normal) : refr;
       factor = ld3(M, 0);  // attenuation = tint
     }
