@@ -577,9 +577,10 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
   double closest = tmax;
   bool hit = false;
   // 1/d of the lane's ray in the current frame (Aabb::hit object.rs:347 divides per test; the
-  // quotient is the same IEEE value every time, so the LANE walker divides once per frame)
+  // quotient is the same value every time, so the LANE walker forms it once per frame, by
+  // rcp_w: within an ulp, and 1/+-0 = +-inf as the slab test needs)
   d3 inv = mk(0., 0., 0.);
-  if (!UNI) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  if (!UNI) inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
 #ifdef RT_PROF
   if (!UNI) PFW(-1, 0);
 #endif
@@ -749,13 +750,13 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
     } else if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y) {
       C.inc(type == RTL_TRANSLATE ? RT_OP_TRANSLATE : RT_OP_ROTATE_Y);
       xform_in(X, o, d);
-      if (!UNI && type == RTL_ROTATE_Y) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+      if (!UNI && type == RTL_ROTATE_Y) inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
       frame = (int)node;
       node = h.w;  // the instance's child
     } else if (type == RTL_EXIT) {
       frame = (int)h.z;
       frame_ray(N, frame, wo, wd, o, d);
-      if (!UNI) inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+      if (!UNI) inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
       node = h.w;
     } else if (MAIN && VOL && type == RTL_VOLUME) {
       // ConstantMedium::hit constant_medium.rs:41-95
@@ -780,12 +781,12 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
         if (t2 > closest) t2 = closest;
         if (t1 < t2) {
           if (t1 < 0.0) t1 = 0.0;
-          double ray_length = sqrt(dot(d, d));
+          double ray_length = sqrt_nr(dot(d, d));
           double dist_inside = (t2 - t1) * ray_length;
           C.inc(RT_OP_VOLUME_DRAWS);
           double hit_distance = ldd(X, 0) * log(rnd(g));
           if (!(hit_distance > dist_inside)) {
-            closest = t1 + hit_distance / ray_length;
+            closest = t1 + div_nr(hit_distance, ray_length);
             hit = true;
             hit_node = node;
             hit_frame = frame;
