@@ -234,6 +234,29 @@ struct Emitter {
     putd(w, p, 4, f[4]), putd(w, p, 5, f[5]), putd(w, p, 6, f[6]);
     putd(w, p, 7, 1.0 / f[3]);  // outward = (p - c) * (1/r)
   }
+  // RTL_VOLF_* when the boundary sequence starting at q has the one-walk form (rt_layout.h)
+  uint32_t fusable_boundary(size_t q) const {
+    auto ty = [&](size_t at) { return at < w.size() ? (w[at] & 0xffu) : 0xffu; };
+    while (ty(q) == RTL_TRANSLATE || ty(q) == RTL_ROTATE_Y) q += RTL_XFORM_WORDS;
+    uint32_t kind = 0;
+    if (ty(q) == RTL_SPHERE) {
+      kind = RTL_VOLF_SPHERE;
+      q += RTL_SPHERE_WORDS;
+    } else if (ty(q) == RTL_QUAD && RTL_QUAD_AXIS(w[q]) != 0u) {
+      kind = RTL_VOLF_QUADS;
+      q += RTL_QUAD_WORDS;
+    } else if (ty(q) == RTL_QUADS) {
+      const uint32_t cnt = w[q] >> 8;
+      q += 4;
+      for (uint32_t k = 0; k < cnt; ++k, q += RTL_QUAD_WORDS)
+        if (ty(q) != RTL_QUAD || RTL_QUAD_AXIS(w[q]) == 0u) return 0u;
+      kind = RTL_VOLF_QUADS;
+    } else {
+      return 0u;
+    }
+    while (ty(q) == RTL_EXIT) q += RTL_EXIT_WORDS;
+    return ty(q) == RTL_END ? kind : 0u;
+  }
   void exit_to(int parent) {
     // Consecutive EXITs collapse into one (restoring straight to the outermost parent) unless
     // a skip link targets the position between them.
@@ -323,6 +346,7 @@ struct Emitter {
         emit(*n.kids[0], frame, chain, true);
         push(RTL_END, RTL_END_WORDS);
         set_skip(p);
+        w[p] |= fusable_boundary(p + RTL_VOLUME_WORDS);
         break;
       }
     }

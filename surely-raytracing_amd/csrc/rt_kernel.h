@@ -371,17 +371,26 @@ __device__ __forceinline__ AQuad load_aquad(Ptr Q) {
   const uint4 a = ld4u(Q), b = ld4u(Q + 4), c = ld4u(Q + 8), e = ld4u(Q + 12);
   return {a.x, hilo(b.x, b.y), hilo(b.z, b.w), hilo(c.x, c.y), hilo(c.z, c.w), hilo(e.x, e.y)};
 }
-template <bool COUNT, int K>
-__device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, double tmin,
-                                           double tmax, double& t_out, Ctr<COUNT>& C) {
+// t and the planar coordinates of an axis-aligned quad (shared by the test below and the
+// one-walk ConstantMedium boundary)
+template <int K>
+__device__ __forceinline__ void aquad_core(const AQuad& q, d3 o, d3 d, d3 r, double& t, double& a,
+                                           double& b) {
   constexpr int LO = K == 0 ? 1 : 0, HI = K == 2 ? 1 : 2;
-  C.inc(RT_OP_QUAD_TESTS);
   const double dk = comp<K>(d), rk = comp<K>(r);
   const double num = q.qk - comp<K>(o);
   const double t0 = num * rk;
-  const double t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
-  const double a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
-  const double b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
+  t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
+  a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
+  b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
+}
+template <bool COUNT, int K>
+__device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, double tmin,
+                                           double tmax, double& t_out, Ctr<COUNT>& C) {
+  C.inc(RT_OP_QUAD_TESTS);
+  const double dk = comp<K>(d);
+  double t, a, b;
+  aquad_core<K>(q, o, d, r, t, a, b);
   // straight-line predicate. a, b in [0, 1] as min/max (IEEE minNum/maxNum): min(a, b) < 0 or
   // 1 < max(a, b) exactly when the reference rejects (object.rs:473), NaN included (a NaN
   // coordinate drops out of min/max, and the reference's comparisons accept it too)
@@ -526,6 +535,91 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
 #pragma unroll
   for (int k = 0; k < RTL_MAX_CHAIN; ++k)
     if ((uint32_t)k < h.z) xform_in(N + c4[k], o, d);
+}
+
+// ConstantMedium::hit's two boundary queries (constant_medium.rs:46-55) in ONE wave-uniform walk
+// of a boundary flagged RTL_VOLF_* by the flattener: rec1 = boundary.hit(r, (-inf, inf)),
+// rec2 = boundary.hit(r, [rec1.t + 1e-4, inf)). With closest-hit updates over one primitive (or
+// a list of quads), rec1.t is the smallest candidate and rec2.t the smallest candidate >= tmin2
+// = rec1.t + 1e-4, where a candidate is a root inside the strict interval (sphere) or a quad
+// hit whose planar coordinates are inside (the quads' interval is inclusive). The walk keeps
+// the two smallest quad candidates (with multiplicity); when both lie below tmin2 the lane
+// needs the third and reports `fallback` (the caller reruns the second query for it). The
+// arithmetic of every candidate is the sphere_test / aquad_test arithmetic, so t1 and t2 are
+// the two-pass values bit for bit. Not used by the op-counting build.
+__device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t kind, d3 o, d3 d,
+                                double tm, double& t1, double& t2, bool& fallback) {
+  const kptr N = (kptr)P.nodes;
+  fallback = false;
+  for (;;) {  // the instance chain in front of the primitive(s)
+    const uint32_t ty = N[node] & 0xffu;
+    if (ty != RTL_TRANSLATE && ty != RTL_ROTATE_Y) break;
+    xform_in(N + node, o, d);
+    node = N[node + 3];
+  }
+  const kptr X = N + node;
+  if (kind == RTL_VOLF_SPHERE) {  // sphere_test's roots once, both strict intervals
+    d3 center = ld3(X, 0);
+    const double r = ldd(X, 3);
+    if (X[0] & RTL_SPHERE_MOVING) center = vfma(tm, ld3(X, 4), center);
+    const d3 oc = o - center;
+    const double a = dot(d, d);
+    const double half_b = dot(oc, d);
+    const double c = dot(oc, oc) - r * r;
+    const double disc = fma(half_b, half_b, -(a * c));
+    const bool real = !(disc < 0.0);
+    const double sqrtd = sqrt_nr(disc);
+    const double ra = rcp_nr(a);
+    const double near = (-half_b - sqrtd) * ra;
+    const double far = (sqrtd - half_b) * ra;
+    const bool n1 = (-kInf < near) & (near < kInf), f1 = (-kInf < far) & (far < kInf);
+    t1 = n1 ? near : far;
+    const double tmin2 = t1 + 0.0001;
+    const bool n2 = (tmin2 < near) & (near < kInf), f2 = (tmin2 < far) & (far < kInf);
+    t2 = n2 ? near : far;
+    return real & (n1 | f1) & (n2 | f2);
+  }
+  // axis-aligned quads: one QUAD record or a QUADS batch
+  const bool batch = (X[0] & 0xffu) == RTL_QUADS;
+  const uint32_t cnt = batch ? (X[0] >> 8) : 1u;
+  kptr Q = batch ? X + 4 : X;
+  const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+  double m1 = 0.0, m2 = 0.0;
+  bool have1 = false, have2 = false;
+  for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
+    const AQuad q = load_aquad(Q);
+    double t, a, b;
+    double dk;
+    switch (RTL_QUAD_AXIS(q.h0)) {
+      case 1u: aquad_core<0>(q, o, d, r, t, a, b); dk = d.x; break;
+      case 2u: aquad_core<1>(q, o, d, r, t, a, b); dk = d.y; break;
+      default: aquad_core<2>(q, o, d, r, t, a, b); dk = d.z; break;
+    }
+    const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+    // aquad_test's predicate without the interval, plus t >= -inf (not NaN)
+    const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);
+    const bool lt1 = v & (!have1 | (t < m1));
+    const bool lt2 = v & !lt1 & (!have2 | (t < m2));
+    m2 = lt1 ? m1 : (lt2 ? t : m2);
+    have2 = have2 | (lt1 & have1) | lt2;
+    m1 = lt1 ? t : m1;
+    have1 = have1 | v;
+  }
+  t1 = m1;
+  const double tmin2 = m1 + 0.0001;
+  bool hit2;
+  if (m1 >= tmin2) {  // only when m1 + 1e-4 rounds back to m1
+    t2 = m1;
+    hit2 = true;
+  } else if (have2 && m2 >= tmin2) {
+    t2 = m2;
+    hit2 = true;
+  } else {
+    t2 = 0.0;
+    hit2 = false;
+    fallback = have2;  // two candidates inside [t1, tmin2): the answer is a third one
+  }
+  return have1 & (hit2 | fallback);
 }
 
 #ifdef RT_PROF
@@ -765,16 +859,34 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       // one rolled loop, so the boundary walker is instantiated once
       double t1 = 0.0, t2 = 0.0;
       bool both = true;
+      const uint32_t fuse = h.x & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
+      if (UNI && !COUNT && fuse) {
+        bool fb;
+        both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+        if (__ballot(fb) != 0ull) {  // rare: rerun the second query for those lanes
+          double tb;
+          uint32_t dn;
+          int df;
+          const bool b2 = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm, o, d,
+                                                                  frame, t1 + 0.0001, kInf, tb,
+                                                                  dn, df, g, C);
+          if (fb) {
+            both = b2;
+            t2 = tb;
+          }
+        }
+      } else {
 #pragma unroll 1
-      for (int pass = 0; pass < 2 && both; ++pass) {
-        double tb;
-        uint32_t dn;
-        int df;
-        both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
-                                                       o, d, frame,
-                                                       pass ? t1 + 0.0001 : -kInf, kInf,
-                                                       tb, dn, df, g, C);
-        if (pass) t2 = tb; else t1 = tb;
+        for (int pass = 0; pass < 2 && both; ++pass) {
+          double tb;
+          uint32_t dn;
+          int df;
+          both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
+                                                         o, d, frame,
+                                                         pass ? t1 + 0.0001 : -kInf, kInf,
+                                                         tb, dn, df, g, C);
+          if (pass) t2 = tb; else t1 = tb;
+        }
       }
       if (both) {
         if (t1 < tmin) t1 = tmin;

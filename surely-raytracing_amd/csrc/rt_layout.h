@@ -82,6 +82,12 @@
 #define RTL_MAX_CHAIN 4
 /* EXIT (4 words): [hdr][skip=unused][parent frame node or -1][next] */
 #define RTL_EXIT_WORDS 4
+/* VOLUME header flags: the boundary is [Translate|RotateY]* then one sphere, or one batch (or
+ * one record) of axis-aligned quads, then EXITs and END; rt_trace then finds both boundary
+ * hits (constant_medium.rs:46-55) in ONE walk (the closest-hit semantics of the two passes
+ * reduce to "smallest candidate" and "smallest candidate >= t1 + 1e-4"). */
+#define RTL_VOLF_SPHERE 0x100u
+#define RTL_VOLF_QUADS 0x200u
 /* VOLUME (8 words): [hdr][skip][mat][next] d0 neg_inv_density, d1 0; the boundary follows and an
  * END node terminates it                                                    constant_medium.rs */
 #define RTL_VOLUME_WORDS 8
