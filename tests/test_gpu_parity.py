@@ -28,6 +28,12 @@ def _gpu(blob, cam, **kw):
 
 def _compare(blob, cam, seed=1, flags=rt.RT_FLAG_OVERWRITE, check_ops=True, **kw):
     acc_g, st = _gpu(blob, cam, seed=seed, flags=flags | rt.RT_FLAG_COUNT_OPS, **kw)
+    # the product kernels (no op counters) take shortcuts the counting build does not: span-1
+    # BVH leaves are tested once (RTL_DUP), ConstantMedium boundaries are queried in one walk
+    # (volume_two_hits). They must reproduce the counting build's image bit for bit.
+    acc_p, _ = _gpu(blob, cam, seed=seed, flags=flags, **kw)
+    assert np.array_equal(acc_p, acc_g, equal_nan=True), \
+        f"product vs counting kernel: max |d| {np.nanmax(np.abs(acc_p - acc_g))}"
     opts = rt.make_opts(cam, seed=seed, flags=flags, **kw)
     acc_o, ops_o = O.render(blob, cam, opts, precision=64)
     spp = cam.samples_per_pixel
@@ -110,6 +116,33 @@ def test_checker_volume_transform_mix(gpu_available):
     blob = sc.serialize(world, lights)
     cam = rt.camera_new(1.0, 80, 16, 20, 45, (0, 3, 8), (0, 1, 0), (0, 1, 0), 0, 0, (0, 0, 0))
     _compare(blob, cam)
+
+
+def test_volume_boundary_one_walk(gpu_available):
+    """ConstantMedium boundaries the flattener marks for the one-walk query: a sphere, and a list
+    of axis-aligned quads (a box with its top face duplicated, so rays through that face have two
+    equal candidates below rec1.t + 1e-4 and take the interpreter fallback for rec2)."""
+    sc = rt.Scene(5)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    light = sc.diffuse_light((8, 8, 8))
+    a, b = (-1.0, 0.0, -1.0), (1.0, 1.5, 1.0)
+    faces = [sc.quad((a[0], a[1], b[2]), (2, 0, 0), (0, 1.5, 0), white),
+             sc.quad((b[0], a[1], b[2]), (0, 0, -2), (0, 1.5, 0), white),
+             sc.quad((b[0], a[1], a[2]), (-2, 0, 0), (0, 1.5, 0), white),
+             sc.quad((a[0], a[1], a[2]), (0, 0, 2), (0, 1.5, 0), white),
+             sc.quad((a[0], b[1], b[2]), (2, 0, 0), (0, 0, -2), white),
+             sc.quad((a[0], b[1], b[2]), (2, 0, 0), (0, 0, -2), white),  # duplicate top
+             sc.quad((a[0], a[1], a[2]), (2, 0, 0), (0, 0, 2), white)]
+    box_fog = sc.constant_medium(sc.rotate_y(sc.hittable_list(*faces), 25), 0.9, (0.9, 0.8, 0.7))
+    ball_fog = sc.constant_medium(sc.sphere((2.0, 0.8, 0.5), 0.8, white), 1.5, (0.3, 0.5, 0.9))
+    floor = sc.quad((-6, -0.01, -6), (12, 0, 0), (0, 0, 12), white)
+    lq = sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light)
+    world = sc.hittable_list(floor, box_fog, ball_fog, lq)
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 72, 16, 12, 40, (0.5, 2.5, 7), (0.3, 0.8, 0), (0, 1, 0), 0, 0, (0.05, 0.05, 0.05))
+    acc_g, _, st = _compare(blob, cam)
+    assert st.op_counts()["volume_draws"] > 0
 
 
 def test_reference_semantics_flag(gpu_available):
