@@ -372,8 +372,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.seed_hi = (uint32_t)(opts->seed >> 32);
   P.tiles_x = (W + kWaveTile - 1) / kWaveTile;
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
-  const int64_t waves_per_sj = (int64_t)P.tiles_x * tiles_y;
-  if ((waves_per_sj * chunk + 3) / 4 > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+  P.n_blk = (S + kPoolSi - 1) / kPoolSi;
+  const int64_t waves_per_sj = (int64_t)P.tiles_x * tiles_y * P.n_blk;  // pools per s_j row
+  if (waves_per_sj * chunk > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
 #ifdef RT_PROF
   const bool count = true;
 #else

@@ -35,6 +35,10 @@ struct cond<false, T, F> {
 };
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 constexpr int kWaveTile = 8;  // 8x8 pixels per wave
+// Stratum columns s_i per pool: a pool is 8x8 pixels x one stratum row s_j x kPoolSi columns,
+// so the last pools of a launch leave at most ~kPoolSi paths per lane of tail (at 961 spp a
+// whole stratum row per pool left ~31: 9 % of an 8-GPU share of the C2 frame).
+constexpr int kPoolSi = 8;
 constexpr int kBlock = 256;   // 4 waves per workgroup
 // BVH kernels run two waves per SIMD (MinWaves below) in ONE 512-thread workgroup per CU, so the
 // workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH region (rt_layout.h).
@@ -206,7 +210,8 @@ struct TraceParams {
   float* __restrict__ samp;  // per-sample radiance, [wave][pool item] x RGB (item = s_i*nv + pv)
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  int n_pools;                       // pools of this launch: tiles x n_sj
+  int n_pools;                       // pools of this launch: tiles x n_sj x n_blk
+  int n_blk;                         // s_i blocks per (tile, s_j): ceil(sqrt_spp / kPoolSi)
   uint32_t root, n_lights, lights_is_list, flags;
   int sphere_light0;    // index of the first SPHERE light record, -1 if none
   double inv_n_lights;  // 1.0 / n_lights (host IEEE division, hittable.rs:116)
@@ -1214,7 +1219,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   // paths) from a global queue and its lanes claim paths across pool boundaries, so lanes only
   // idle at the very end of the launch. Wave-uniform pool state:
   const int lane = threadIdx.x & 63;
-  int pool_id = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_j = 0;
+  // pool = (tile, s_j, block of kPoolSi stratum columns s_i); tsj = tile * n_sj + s_j index
+  int tsj = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_j = 0;
   bool more = true;  // the queue may still hold pools
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
@@ -1238,14 +1244,16 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       if (lane == 0) id = atomicAdd(P.queue, 1u);
       id = __builtin_amdgcn_readfirstlane(id);
       if ((int)id < P.n_pools) {
-        pool_id = (int)id;
-        const int tile = pool_id / P.n_sj;
+        const int blk = (int)id % P.n_blk;
+        tsj = (int)id / P.n_blk;
+        const int tile = tsj / P.n_sj;
         tx = tile % P.tiles_x;
         ty = tile / P.tiles_x;
         tile_w = imin(kWaveTile, P.W - tx * kWaveTile);
         nv = tile_w * imin(kWaveTile, P.n_rows - ty * kWaveTile);
-        pool = nv * P.sqrt_spp;
-        s_j = P.sj0 + pool_id % P.n_sj;
+        si0 = blk * kPoolSi;
+        pool = nv * imin(kPoolSi, P.sqrt_spp - si0);
+        s_j = P.sj0 + tsj % P.n_sj;
       } else {
         more = false;
         pool = 0;
@@ -1260,12 +1268,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         int pv, s_i, px_, py_;
         if (nv == kWaveTile * kWaveTile) {  // full tile (wave-uniform): shifts
           pv = k & (kWaveTile * kWaveTile - 1);
-          s_i = k >> 6;
+          s_i = si0 + (k >> 6);
           px_ = pv & (kWaveTile - 1);
           py_ = pv >> 3;
         } else {
           pv = k % nv;
-          s_i = k / nv;
+          s_i = si0 + k / nv;
           px_ = pv % tile_w;
           py_ = pv / tile_w;
         }
@@ -1273,7 +1281,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         const int x = tx * kWaveTile + px_;
         const int kr = ty * kWaveTile + py_;
         const int y = Q->row_begin + kr * Q->row_step;
-        slot = (size_t)pool_id * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + k;
+        // slot order of (tile, s_j): s_i * nv + pv (rt_reduce), whatever the s_i block
+        slot = (size_t)tsj * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + (size_t)(s_i * nv + pv);
         // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
         g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
                      (uint32_t)(s_j * Q->sqrt_spp + s_i));
