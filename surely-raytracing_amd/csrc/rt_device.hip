@@ -45,31 +45,36 @@ __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::valu
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
-// order of render.rs:185-189, in f64. Samples sit in pool-item order per wave (item =
-// s_i * nv + pv), so neighbouring pixels read neighbouring slots. Chunked calls carry the
-// running sum in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite.
+// order of render.rs:185-189, in f64. One wave per 8x8 tile, lane = pixel of the tile: the
+// samples of one (tile, s_j, s_i) sit in pool-item order (item = s_i * nv + pv), so every load
+// instruction reads nv * 12 contiguous bytes. Chunked calls carry the running sum in `tot`.
+// mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite.
 __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
                                                  double* __restrict__ tot,
                                                  float* __restrict__ accum, int W, int n_rows,
-                                                 int tiles_x, int n_sj, int S, int mode) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= W * n_rows) return;
-  const int x = i % W, kr = i / W;
-  const int tx = x / kWaveTile, ty = kr / kWaveTile;
+                                                 int tiles_x, int n_tiles, int n_sj, int S,
+                                                 int mode) {
+  const int tile_id = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int pv = threadIdx.x & 63;
+  if (tile_id >= n_tiles) return;
+  const int tx = tile_id % tiles_x, ty = tile_id / tiles_x;
   const int tile_w = min(kWaveTile, W - tx * kWaveTile);
   const int tile_h = min(kWaveTile, n_rows - ty * kWaveTile);
   const int nv = tile_w * tile_h;
-  const int pv = (kr - ty * kWaveTile) * tile_w + (x - tx * kWaveTile);
-  const size_t tile = (size_t)ty * tiles_x + tx;
+  if (pv >= nv) return;
+  const int x = tx * kWaveTile + pv % tile_w, kr = ty * kWaveTile + pv / tile_w;
+  const size_t i = (size_t)kr * W + x;
+  const size_t tile = (size_t)tile_id;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   if (!(mode & 1)) {
-    t0 = tot[3 * (size_t)i];
-    t1 = tot[3 * (size_t)i + 1];
-    t2 = tot[3 * (size_t)i + 2];
+    t0 = tot[3 * i];
+    t1 = tot[3 * i + 1];
+    t2 = tot[3 * i + 2];
   }
   for (int k = 0; k < n_sj; ++k) {
     const float* r = samp + ((tile * n_sj + k) * (size_t)(kWaveTile * kWaveTile) * S + pv) * 3;
     double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll 8
     for (int si = 0; si < S; ++si) {
       const float* q = r + (size_t)si * nv * 3;
       r0 += (double)q[0];
@@ -80,7 +85,7 @@ __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
     t1 += r1;
     t2 += r2;
   }
-  float* a = accum + 3 * (size_t)i;
+  float* a = accum + 3 * i;
   if (mode & 2) {
     if (mode & 4) {
       a[0] = (float)t0, a[1] = (float)t1, a[2] = (float)t2;
@@ -89,7 +94,7 @@ __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
       a[2] = (float)((double)a[2] + t2);
     }
   } else {
-    tot[3 * (size_t)i] = t0, tot[3 * (size_t)i + 1] = t1, tot[3 * (size_t)i + 2] = t2;
+    tot[3 * i] = t0, tot[3 * i + 1] = t1, tot[3 * i + 2] = t2;
   }
 }
 
@@ -438,8 +443,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     ++sc->n_tev;
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
                      ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
-    hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_px + 255) / 256)), dim3(256), 0, stream, samp,
-                       tot, accum, W, opts->n_rows, P.tiles_x, cn, S, mode);
+    const int n_tiles = P.tiles_x * tiles_y;
+    hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, stream, samp,
+                       tot, accum, W, opts->n_rows, P.tiles_x, n_tiles, cn, S, mode);
     HIP_TRY(hipGetLastError());
   }
   ++sc->n_render;
