@@ -194,6 +194,12 @@ int rt_device_count(int* count);
 /* Validate a blob without touching a device (hittable/object invariants, tag and index ranges). */
 int rt_scene_validate(const rt_scene_blob* blob);
 
+/* Host-only diagnostics of the flattened layout (no device needed): out[0..7] = node words,
+ * BVH-region words, BVH records, DUP records (span-1 leaves tested once), ConstantMedium
+ * records, of which one-walk sphere / one-walk quad boundaries, and light records. */
+#define RT_LAYOUT_STATS 8
+int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n);
+
 /* Validate, flatten (threaded node array, f64 payloads; rt_layout.h) and upload to `device`. */
 int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* scene);

@@ -163,6 +163,28 @@ int rt_scene_validate(const rt_scene_blob* blob) {
   return RT_OK;
 }
 
+int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n) {
+  if (!out || n < 0) return set_err(RT_ERR_INVALID_ARG, "null out");
+  rtf::FlatScene F;
+  std::string err;
+  int rc = rtf::flatten(blob, &F, &err);
+  if (rc != RT_OK) return set_err(rc, err);
+  uint32_t v[RT_LAYOUT_STATS] = {(uint32_t)F.nodes.size(), F.hdr.bvh_words, 0, 0, 0, 0, 0,
+                                 F.hdr.n_lights};
+  for (size_t p = 0; p < F.nodes.size(); p += rtf::record_words(F.nodes[p])) {
+    const uint32_t h = F.nodes[p], ty = h & 0xffu;
+    if (ty == RTL_BVH) ++v[2];
+    if (ty == RTL_DUP) ++v[3];
+    if (ty == RTL_VOLUME) {
+      ++v[4];
+      if (h & RTL_VOLF_SPHERE) ++v[5];
+      if (h & RTL_VOLF_QUADS) ++v[6];
+    }
+  }
+  for (int k = 0; k < n && k < RT_LAYOUT_STATS; ++k) out[k] = v[k];
+  return RT_OK;
+}
+
 int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   if (!out) return set_err(RT_ERR_INVALID_ARG, "null out");
   *out = nullptr;

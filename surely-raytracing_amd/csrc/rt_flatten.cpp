@@ -361,6 +361,8 @@ bool tex_needs_uv(const std::vector<uint32_t>& texs, uint32_t id, int depth) {
   return false;
 }
 
+}  // namespace
+
 // Words of the record starting with header word h.
 uint32_t record_words(uint32_t h) {
   switch (h & 0xffu) {
@@ -375,6 +377,8 @@ uint32_t record_words(uint32_t h) {
     default: return 4;  // END, QUADS header
   }
 }
+
+namespace {
 
 // Move every BVH record to the front of the node array (the BVH region [0, bvh_words), staged
 // in LDS by rt_trace) and make every link explicit (rt_layout.h): BVH records get their first

@@ -21,6 +21,9 @@ struct FlatScene {
   std::vector<uint8_t> texels;
 };
 
+// Words of the node record starting with header word h (rt_layout.h).
+uint32_t record_words(uint32_t h);
+
 // Returns RT_OK or a negative rt status; *err explains failures.
 int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err);
 

@@ -183,6 +183,8 @@ def load_device_lib(path: Path) -> C.CDLL:
         "rt_render_blob": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
                                      C.POINTER(RtRenderOpts), C.c_void_p,
                                      C.POINTER(RtStats)]),
+        "rt_scene_layout_stats": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(C.c_uint32),
+                                            C.c_int]),
         "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
                                         C.POINTER(C.c_int)]),
     }
@@ -466,6 +468,17 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
     finally:
         ds.close()
     return accum, st
+
+
+LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
+                "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights"]
+
+
+def layout_stats(blob: "Blob") -> dict:
+    """Host-only counts of the flattened device layout (rt_scene_layout_stats)."""
+    out = (C.c_uint32 * len(LAYOUT_STATS))()
+    _check_dev(device_lib().rt_scene_layout_stats(blob.ref(), out, len(LAYOUT_STATS)))
+    return dict(zip(LAYOUT_STATS, (int(v) for v in out)))
 
 
 def device_count() -> int:
