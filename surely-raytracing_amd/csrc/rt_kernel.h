@@ -100,6 +100,13 @@ __device__ __forceinline__ double rcp_nr(double b) {
   r = fma(fma(-b, r, 1.0), r, r);
   return fma(fma(-b, r, 1.0), r, r);
 }
+// The per-batch reciprocal of an axis-aligned quad test: one Newton step. The test's quotient
+// is then corrected once more (t = t0 + (num - d t0) r, aquad_core), which is what bounds t to
+// an ulp; the second step of rcp_nr would only refine r below that.
+__device__ __forceinline__ double rcp_nr1(double b) {
+  const double r = __builtin_amdgcn_rcp(b);
+  return fma(fma(-b, r, 1.0), r, r);
+}
 __device__ __forceinline__ double div_nr(double a, double b) {
   double r = rcp_nr(b);
   double q = a * r;
@@ -588,7 +595,7 @@ __device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t ki
   const bool batch = (X[0] & 0xffu) == RTL_QUADS;
   const uint32_t cnt = batch ? (X[0] >> 8) : 1u;
   kptr Q = batch ? X + 4 : X;
-  const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
   double m1 = 0.0, m2 = 0.0;
   bool have1 = false, have2 = false;
   for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
@@ -745,7 +752,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
     uint32_t type = h.x & 0xffu;
     if (type == RTL_QUAD) {
       double t = closest;
-      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+      const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
       bool hq;
       if (UNI) {
         hq = world_quad_test<COUNT>(X, o, d, r, tmin, closest, t, C);
@@ -765,7 +772,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       // batch of sibling quads: the same sequential closest-hit updates as the list
       const uint32_t cnt = h.x >> 8;
       Ptr Q = X + 4;
-      const d3 r = mk(rcp_nr(d.x), rcp_nr(d.y), rcp_nr(d.z));
+      const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
       uint4 a0, a1, a2, a3;  // LANE: the next quad's axis form is in flight during this test
       if (!UNI) ld64(Q, a0, a1, a2, a3);
       // the batch's winner is tracked as an index: one select per quad instead of three
@@ -1088,11 +1095,11 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
         const kdptr A = reinterpret_cast<kdptr>(L + 4) + RTL_LQUAD_AXIS_D;
         const AQuad q = {L[0], A[0], A[1], A[2], A[3], A[4]};
         if (axis == 1u) {
-          hq = aquad_test<COUNT, 0>(q, origin, dir, mk(rcp_nr(dir.x), 0., 0.), 0.001, kInf, t, C);
+          hq = aquad_test<COUNT, 0>(q, origin, dir, mk(rcp_nr1(dir.x), 0., 0.), 0.001, kInf, t, C);
         } else if (axis == 2u) {
-          hq = aquad_test<COUNT, 1>(q, origin, dir, mk(0., rcp_nr(dir.y), 0.), 0.001, kInf, t, C);
+          hq = aquad_test<COUNT, 1>(q, origin, dir, mk(0., rcp_nr1(dir.y), 0.), 0.001, kInf, t, C);
         } else {
-          hq = aquad_test<COUNT, 2>(q, origin, dir, mk(0., 0., rcp_nr(dir.z)), 0.001, kInf, t, C);
+          hq = aquad_test<COUNT, 2>(q, origin, dir, mk(0., 0., rcp_nr1(dir.z)), 0.001, kInf, t, C);
         }
       } else {
         hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
