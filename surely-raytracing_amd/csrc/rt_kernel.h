@@ -38,7 +38,10 @@ constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 // Stratum columns s_i per pool: a pool is 8x8 pixels x one stratum row s_j x kPoolSi columns,
 // so the last pools of a launch leave at most ~kPoolSi paths per lane of tail (at 961 spp a
 // whole stratum row per pool left ~31: 9 % of an 8-GPU share of the C2 frame).
-constexpr int kPoolSi = 8;
+#ifndef RT_POOL_SI
+#define RT_POOL_SI 8
+#endif
+constexpr int kPoolSi = RT_POOL_SI;
 constexpr int kBlock = 256;   // 4 waves per workgroup
 // BVH kernels run two waves per SIMD (MinWaves below) in ONE 512-thread workgroup per CU, so the
 // workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH region (rt_layout.h).

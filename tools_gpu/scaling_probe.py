@@ -4,6 +4,10 @@ import sys
 sys.path.insert(0, "surely-raytracing_amd")
 import numpy as np  # noqa: E402
 import surely_rt as rt  # noqa: E402
+import os  # noqa: E402
+
+if os.environ.get("RT_LIB"):  # a library variant (tools only)
+    rt._dev = rt.load_device_lib(os.environ["RT_LIB"])
 from surely_rt.parallel import cyclic_rows  # noqa: E402
 
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 800
