@@ -145,6 +145,40 @@ def test_volume_boundary_one_walk(gpu_available):
     assert st.op_counts()["volume_draws"] > 0
 
 
+def test_bvh_over_instances_volumes_and_general_quads(gpu_available):
+    """A BvhNode tree whose leaves are instanced boxes (Translate/RotateY inside the per-lane
+    walker: frame changes, EXIT links, 1/d recomputed), a ConstantMedium (never elided as a
+    duplicate: it draws), non-axis-aligned quads (the general quad test), moving spheres and
+    spheres; 5 and 7 leaves give span-1 nodes, i.e. DUP records over each kind of subtree."""
+    sc = rt.Scene(21)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    red = sc.lambertian((0.65, 0.05, 0.05))
+    glass = sc.dielectric(1.5)
+    light = sc.diffuse_light((10, 10, 10))
+    items = sc.hittable_list()
+    for k in range(7):
+        x = -3.0 + k
+        if k % 3 == 0:
+            sc.add(items, sc.translate(sc.rotate_y(sc.make_box((0, 0, 0), (0.6, 0.9, 0.6), red),
+                                                   15 * k), (x, 0, -0.3)))
+        elif k % 3 == 1:
+            sc.add(items, sc.quad((x, 0.1, 0.5), (0.5, 0.4, 0.0), (0.0, 0.3, 0.6), white))
+        else:
+            sc.add(items, sc.sphere_moving((x, 0.4, 0), (x, 0.6, 0.1), 0.3, glass))
+    sc.add(items, sc.constant_medium(sc.sphere((0.5, 1.5, 0.2), 0.5, white), 2.0, (0.8, 0.8, 0.9)))
+    sc.add(items, sc.sphere((1.5, 1.4, -0.5), 0.35, white))
+    inner = sc.create_bvh(items)
+    world = sc.hittable_list(sc.quad((-6, -0.01, -6), (12, 0, 0), (0, 0, 12), white),
+                             sc.translate(sc.rotate_y(inner, -10), (0.2, 0, 0)),
+                             sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    st = rt.layout_stats(blob)
+    assert st["bvh_records"] > 0 and st["dup_records"] > 0
+    cam = rt.camera_new(1.0, 72, 16, 20, 40, (0.5, 2.0, 8), (0, 0.6, 0), (0, 1, 0), 0, 0, (0.1, 0.1, 0.12))
+    _compare(blob, cam)
+
+
 def test_reference_semantics_flag(gpu_available):
     """RT_FLAG_SEMANTICS_REFERENCE: empty light list + diffuse material is an error, as the
     reference panics (hittable.rs:115-129 via render.rs:140-142)."""
