@@ -1116,8 +1116,24 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
       }
     } else if (type == RTL_SPHERE) {
       C.inc(RT_OP_LIGHT_PDF_SPHERE);
-      double t = 0.0;
-      const bool hs = sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C);
+      bool hs;
+      if (COUNT) {
+        double t = 0.0;
+        hs = sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C);
+      } else {
+        // Only a weight depends on this test (a PDF value), so the product build asks the same
+        // question without the root: some root of Sphere::hit lies in (0.001, inf) exactly when
+        // the far root does, (sqrt(disc) - half_b) / a > 0.001, i.e. sqrt(disc) > c1 = 0.001 a +
+        // half_b: true for c1 < 0, else disc > c1^2 (object.rs:145-166 at time 0, 193).
+        const d3 oc = origin - ld3(L, 0);
+        const double a = dot(dir, dir);
+        const double half_b = dot(oc, dir);
+        const double r = ldd(L, 3);
+        const double c = dot(oc, oc) - r * r;
+        const double disc = fma(half_b, half_b, -(a * c));
+        const double c1 = fma(0.001, a, half_b);
+        hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));
+      }
       double cos_max = 0.0;
       if ((int)i == P.sphere_light0) {  // uniform: the shared value (straight-line)
         cos_max = cos_sl0;
@@ -1296,6 +1312,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
         g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
                      (uint32_t)(s_j * Q->sqrt_spp + s_i));
+#ifdef RT_ABL_SEED2  // ablation build: the per-sample RNG seeding (pcg4d) done twice
+        {
+          uint32_t xx = (uint32_t)x;
+          asm volatile("" : "+v"(xx));
+          const Rng g2 = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + (int)xx),
+                                  (uint32_t)(s_j * Q->sqrt_spp + s_i));
+          asm volatile("" ::"v"(g2.s0), "v"(g2.s1), "v"(g2.s2), "v"(g2.s3));
+        }
+#endif
         C.inc(RT_OP_SAMPLES);
         d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
         double px = fma(Q->rs, (double)s_i + rnd(g), -0.5);
@@ -1370,6 +1395,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     uint32_t type = X[0] & 0xffu;
     d3 o, d;
     frame_ray(T.nodes, hf, ro, rd, o, d);
+#ifdef RT_ABL_HIT2  // ablation build: the hit record's frame recomputed (transform chain) twice
+    {
+      d3 o2, d2, ro2 = ro;
+      asm volatile("" : "+v"(ro2.x));
+      frame_ray(T.nodes, hf, ro2, rd, o2, d2);
+      asm volatile("" ::"v"(o2.x), "v"(o2.y), "v"(o2.z), "v"(d2.x), "v"(d2.y), "v"(d2.z));
+    }
+#endif
     d3 p = vfma(t, d, o);
     d3 normal;
     bool front = true;
@@ -1535,6 +1568,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
       if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, cos_sl, C), 0.5 * mat_pdf);  // pdf.rs:116
+#ifdef RT_ABL_LPDF2  // ablation build: the light PDF evaluated twice (same result)
+      if (have_lights) {
+        d3 p2 = p;
+        asm volatile("" : "+v"(p2.x));
+        const double lp2 = light_pdf<COUNT>(P, p2, dir, cos_sl, C);
+        asm volatile("" ::"v"(lp2));
+      }
+#endif
 #endif
       PROF(6);
       factor = atten * (s_pdf * rcp_w(pdf_val));
