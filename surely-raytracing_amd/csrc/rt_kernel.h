@@ -43,9 +43,14 @@ constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 #endif
 constexpr int kPoolSi = RT_POOL_SI;
 constexpr int kBlock = 256;   // 4 waves per workgroup
-// BVH kernels run two waves per SIMD (MinWaves below) in ONE 512-thread workgroup per CU, so the
-// workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH region (rt_layout.h).
-constexpr int kBlockBvh = 512;
+// BVH kernels run three waves per SIMD (MinWaves below: <= 168 VGPRs) in ONE 768-thread
+// workgroup per CU, so the workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH
+// region (rt_layout.h). final_scene: 416 Msamples/s at 512 threads x 2 waves, 443 at 1024 x 4
+// (spilling), 523 at 768 x 3 (tools_gpu/ab_variants.py).
+#ifndef RT_BLOCK_BVH
+#define RT_BLOCK_BVH 768
+#endif
+constexpr int kBlockBvh = RT_BLOCK_BVH;
 template <bool BVH>
 struct BlockOf {
   static constexpr int value = BVH ? kBlockBvh : kBlock;
@@ -53,15 +58,14 @@ struct BlockOf {
 // Dynamic LDS budgets: whole small scenes (kStageScene) / the BVH region of a BVH kernel.
 constexpr size_t kLdsBvhMax = 152u << 10;
 // Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument). 4 caps the
-// allocation at 128 VGPRs. Kernels with a per-lane BVH walker need more than that without
-// spilling inside the walk, and spills there cost more than the occupancy they buy: 2 waves
-// (256 VGPRs) measured 294 vs 214 Msamples/s on final_scene; volume/texture kernels without a
-// BVH stay at 4 (cornell_smoke: 2221 at 4 vs 1985 at 2). tools_gpu/ab_variants.py, variants-occ.
+// allocation at 128 VGPRs. Kernels with a per-lane BVH walker run 3 (168 VGPRs; see kBlockBvh);
+// kernels without a BVH stay at 4 (cornell_box at 3 or 5: -13 %; cornell_smoke at 3: -8 %,
+// at 5: -12 %). tools_gpu/ab_variants.py.
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 4
 #endif
 #ifndef RT_MIN_WAVES_BVH
-#define RT_MIN_WAVES_BVH 2
+#define RT_MIN_WAVES_BVH 3
 #endif
 template <bool VOL, bool TEX, bool BVH>
 struct MinWaves {
