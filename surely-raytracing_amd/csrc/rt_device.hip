@@ -38,10 +38,10 @@ using namespace rtk;
 namespace {
 
 // Ahead-of-time kernels: the interpreter traversal, one per feature combination.
-template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB = VOL>
 __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(
     TraceParams P) {
-  trace_body<COUNT, VOL, TEX, BVH, STAGED, TravInterp>(P);
+  trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, TravInterp>(P);
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
@@ -130,8 +130,8 @@ struct rt_scene {
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
-  int resident_blocks[32] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
-  size_t resident_lds[32] = {};  // ... at this dynamic LDS size
+  int resident_blocks[40] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
+  size_t resident_lds[40] = {};  // ... at this dynamic LDS size
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -432,21 +432,31 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const bool staged = !bvh && P.stage_scene;
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
                    (bvh ? 1 : 0) + (staged ? 16 : 0);
-  kern_t kern = staged ? table_staged[kidx / 2 - 8] : table[kidx];
+  // BVH scenes whose volumes all sit outside BVH subtrees (final_scene) run the variant whose
+  // per-lane walker has no volume branch
+  static const kern_t table_bvh_novolb[8] = {
+      rt_trace<false, true, false, true, false, false>, rt_trace<false, true, true, true, false, false>,
+      rt_trace<true, true, false, true, false, false>,  rt_trace<true, true, true, true, false, false>,
+      nullptr, nullptr, nullptr, nullptr};
+  const bool novolb = bvh && vol && !sc->hdr.volume_in_bvh;
+  kern_t kern = staged ? table_staged[kidx / 2 - 8]
+                       : (novolb ? table_bvh_novolb[(kidx >= 8 ? 2 : 0) + (tex ? 1 : 0)]
+                                 : table[kidx]);
+  const int kslot = novolb ? 32 + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0) : kidx;
   const int block = bvh ? kBlockBvh : kBlock;
   if (lds_bytes > (64u << 10))
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_bytes));
-  if (sc->resident_blocks[kidx] == 0 || sc->resident_lds[kidx] != lds_bytes) {
+  if (sc->resident_blocks[kslot] == 0 || sc->resident_lds[kslot] != lds_bytes) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, block, lds_bytes) !=
             hipSuccess ||
         nb <= 0)
       nb = 1;
-    sc->resident_blocks[kidx] = nb;
-    sc->resident_lds[kidx] = lds_bytes;
+    sc->resident_blocks[kslot] = nb;
+    sc->resident_lds[kslot] = lds_bytes;
   }
-  const int64_t max_blocks = (int64_t)sc->resident_blocks[kidx] * std::max(1, sc->n_cu);
+  const int64_t max_blocks = (int64_t)sc->resident_blocks[kslot] * std::max(1, sc->n_cu);
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
     const int cn = std::min(chunk, sj0 + n_sj - c0);
     P.sj0 = c0;

@@ -144,7 +144,8 @@ struct Emitter {
   std::string err;
   int status = RT_OK;
   uint32_t max_chain = 0;
-  bool has_bvh = false, has_volume = false;
+  bool has_bvh = false, has_volume = false, volume_in_bvh = false;
+  int bvh_depth = 0;  // BVH subtrees enclosing the record being emitted
   size_t last_exit_end = (size_t)-1;  // end position of the most recent EXIT node
   size_t last_skip_target = (size_t)-1;
 
@@ -297,6 +298,7 @@ struct Emitter {
         has_bvh = true;
         size_t p = push(RTL_BVH, RTL_BVH_WORDS);
         for (int k = 0; k < 6; ++k) putd(w, p, k, n.bbox[k]);
+        ++bvh_depth;
         emit(*n.kids[0], frame, chain, in_volume);
         if (same_tree(*n.kids[0], *n.kids[1]) && !has_volume_node(*n.kids[1])) {
           size_t d = push(RTL_DUP, RTL_DUP_WORDS);
@@ -305,6 +307,7 @@ struct Emitter {
         } else {
           emit(*n.kids[1], frame, chain, in_volume);
         }
+        --bvh_depth;
         set_skip(p);
         break;
       }
@@ -340,6 +343,7 @@ struct Emitter {
         }
         if (!check_mat(n.mat)) return;
         has_volume = true;
+        if (bvh_depth > 0) volume_in_bvh = true;
         size_t p = push(RTL_VOLUME, RTL_VOLUME_WORDS);
         w[p + 2] = (uint32_t)n.mat;
         putd(w, p, 0, n.f[0]);
@@ -640,6 +644,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.lights_is_list = is_list;
   h.has_bvh = em.has_bvh;
   h.has_volume = em.has_volume;
+  h.volume_in_bvh = em.volume_in_bvh;
   h.max_chain = em.max_chain;
   h.n_texel_bytes = (uint32_t)n_texel;
   h.pdf_materials = pdf_mats;

@@ -680,7 +680,9 @@ __device__ __forceinline__ bool prof_first_lane() {
 //       independent 16-byte vector loads, so one memory round trip serves a BVH node. The UNI
 //       walker hands a BVH subtree [root, skip) to the LANE walker with the current closest-hit
 //       state and resumes at its skip once every lane has finished it (BVH = the scene has one).
-template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH>
+// VOLB: some ConstantMedium lies inside a BVH subtree (the per-lane walker then needs its volume
+// branch, a nested walker; without it the LANE instantiation leaves that code out).
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL>
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
                          double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
@@ -829,7 +831,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
           const unsigned long long pt0 = __builtin_readcyclecounter();
           prof_steps[threadIdx.x] = 0u;
 #endif
-          const bool sub = traverse<MAIN, COUNT, VOL, false, BVH>(P, node, h.y, wo, wd, tm, o, d,
+          const bool sub = traverse<MAIN, COUNT, VOLB, false, BVH>(P, node, h.y, wo, wd, tm, o, d,
                                                                  frame, tmin, closest, t, hn, hf,
                                                                  g, C);
 #ifdef RT_PROF
@@ -1168,18 +1170,18 @@ __device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t sl
 // the run-time interpreter of the flattened node sequence. Scene-specialised kernels (rt_jit.cpp)
 // supply a generated policy with the same signature and the same arithmetic.
 struct TravInterp {
-  template <bool COUNT, bool VOL, bool BVH>
+  template <bool COUNT, bool VOL, bool BVH, bool VOLB>
   static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,
                                                double& t, uint32_t& hn, int& hf, Rng& g,
                                                Ctr<COUNT>& C) {
-    return traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001,
-                                                 kInf, t, hn, hf, g, C);
+    return traverse<true, COUNT, VOL, true, BVH, VOLB>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1,
+                                                       0.0001, kInf, t, hn, hf, g, C);
   }
 };
 
 // The path kernel body; instantiated by rt_device.hip (interpreter) and by scene-specialised
 // JIT kernels. Its __global__ wrapper passes TraceParams as the only kernel argument (kparams()).
-template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, class Trav>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB, class Trav>
 __device__ __forceinline__ void trace_body(const TraceParams& P) {
   // STAGED: the small-table prefix is in LDS (P.stage_scene) and per-lane table reads are
   // ds_reads through 32-bit LDS pointers; otherwise they read the global tables.
@@ -1386,7 +1388,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
     }
 #endif
-    if (!Trav::template world<COUNT, VOL, BVH>(P, ro, rd, tm, t, hn, hf, g, C)) {
+    if (!Trav::template world<COUNT, VOL, BVH, VOLB>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * karr3(kparams()->bg);
       store_sample(P.samp, slot, Lp);
