@@ -38,10 +38,11 @@ using namespace rtk;
 namespace {
 
 // Ahead-of-time kernels: the interpreter traversal, one per feature combination.
-template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB = VOL>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB = VOL,
+          bool VOLI = true>
 __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(
     TraceParams P) {
-  trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, TravInterp>(P);
+  trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterp>(P);
 }
 
 // Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
@@ -433,16 +434,21 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
                    (bvh ? 1 : 0) + (staged ? 16 : 0);
   // BVH scenes whose volumes all sit outside BVH subtrees (final_scene) run the variant whose
-  // per-lane walker has no volume branch
+  // per-lane walker has no volume branch; when those volumes are all one-walk spheres, the
+  // top-level walker carries no two-walk interpreter either
   static const kern_t table_bvh_novolb[8] = {
       rt_trace<false, true, false, true, false, false>, rt_trace<false, true, true, true, false, false>,
       rt_trace<true, true, false, true, false, false>,  rt_trace<true, true, true, true, false, false>,
-      nullptr, nullptr, nullptr, nullptr};
+      rt_trace<false, true, false, true, false, false, false>,
+      rt_trace<false, true, true, true, false, false, false>,
+      rt_trace<true, true, false, true, false, false, false>,
+      rt_trace<true, true, true, true, false, false, false>};
   const bool novolb = bvh && vol && !sc->hdr.volume_in_bvh;
-  kern_t kern = staged ? table_staged[kidx / 2 - 8]
-                       : (novolb ? table_bvh_novolb[(kidx >= 8 ? 2 : 0) + (tex ? 1 : 0)]
-                                 : table[kidx]);
-  const int kslot = novolb ? 32 + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0) : kidx;
+  // the op-counting build always walks twice, so only product kernels drop the interpreter
+  const bool novoli = novolb && sc->hdr.volumes_one_walk_spheres && !(opts->flags & RT_FLAG_COUNT_OPS);
+  const int vb = (novoli ? 4 : 0) + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0);
+  kern_t kern = staged ? table_staged[kidx / 2 - 8] : (novolb ? table_bvh_novolb[vb] : table[kidx]);
+  const int kslot = novolb ? 32 + vb : kidx;
   const int block = bvh ? kBlockBvh : kBlock;
   if (lds_bytes > (64u << 10))
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,

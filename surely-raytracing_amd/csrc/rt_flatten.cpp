@@ -144,7 +144,7 @@ struct Emitter {
   std::string err;
   int status = RT_OK;
   uint32_t max_chain = 0;
-  bool has_bvh = false, has_volume = false, volume_in_bvh = false;
+  bool has_bvh = false, has_volume = false, volume_in_bvh = false, all_sphere_volumes = true;
   int bvh_depth = 0;  // BVH subtrees enclosing the record being emitted
   size_t last_exit_end = (size_t)-1;  // end position of the most recent EXIT node
   size_t last_skip_target = (size_t)-1;
@@ -351,6 +351,7 @@ struct Emitter {
         push(RTL_END, RTL_END_WORDS);
         set_skip(p);
         w[p] |= fusable_boundary(p + RTL_VOLUME_WORDS);
+        if (!(w[p] & RTL_VOLF_SPHERE)) all_sphere_volumes = false;
         break;
       }
     }
@@ -645,6 +646,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.has_bvh = em.has_bvh;
   h.has_volume = em.has_volume;
   h.volume_in_bvh = em.volume_in_bvh;
+  h.volumes_one_walk_spheres = em.has_volume && em.all_sphere_volumes;
   h.max_chain = em.max_chain;
   h.n_texel_bytes = (uint32_t)n_texel;
   h.pdf_materials = pdf_mats;

@@ -682,7 +682,9 @@ __device__ __forceinline__ bool prof_first_lane() {
 //       state and resumes at its skip once every lane has finished it (BVH = the scene has one).
 // VOLB: some ConstantMedium lies inside a BVH subtree (the per-lane walker then needs its volume
 // branch, a nested walker; without it the LANE instantiation leaves that code out).
-template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL>
+// VOLI: some ConstantMedium boundary may need the interpreter's two walks (not one-walk, or one-
+// walk quads whose third candidate can be needed); without it only volume_two_hits is compiled.
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL, bool VOLI = true>
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
                          double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
@@ -881,7 +883,10 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       double t1 = 0.0, t2 = 0.0;
       bool both = true;
       const uint32_t fuse = h.x & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
-      if (UNI && !COUNT && fuse) {
+      if constexpr (UNI && !COUNT && !VOLI) {  // every boundary is a one-walk sphere
+        bool fb;
+        both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+      } else if (UNI && !COUNT && fuse) {
         bool fb;
         both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
         if (__ballot(fb) != 0ull) {  // rare: rerun the second query for those lanes
@@ -1170,18 +1175,18 @@ __device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t sl
 // the run-time interpreter of the flattened node sequence. Scene-specialised kernels (rt_jit.cpp)
 // supply a generated policy with the same signature and the same arithmetic.
 struct TravInterp {
-  template <bool COUNT, bool VOL, bool BVH, bool VOLB>
+  template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>
   static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,
                                                double& t, uint32_t& hn, int& hf, Rng& g,
                                                Ctr<COUNT>& C) {
-    return traverse<true, COUNT, VOL, true, BVH, VOLB>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1,
-                                                       0.0001, kInf, t, hn, hf, g, C);
+    return traverse<true, COUNT, VOL, true, BVH, VOLB, VOLI>(P, P.root, ~0u, ro, rd, tm, ro, rd,
+                                                             -1, 0.0001, kInf, t, hn, hf, g, C);
   }
 };
 
 // The path kernel body; instantiated by rt_device.hip (interpreter) and by scene-specialised
 // JIT kernels. Its __global__ wrapper passes TraceParams as the only kernel argument (kparams()).
-template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB, class Trav>
+template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB, bool VOLI, class Trav>
 __device__ __forceinline__ void trace_body(const TraceParams& P) {
   // STAGED: the small-table prefix is in LDS (P.stage_scene) and per-lane table reads are
   // ds_reads through 32-bit LDS pointers; otherwise they read the global tables.
@@ -1388,7 +1393,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
     }
 #endif
-    if (!Trav::template world<COUNT, VOL, BVH, VOLB>(P, ro, rd, tm, t, hn, hf, g, C)) {
+    if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * karr3(kparams()->bg);
       store_sample(P.samp, slot, Lp);
