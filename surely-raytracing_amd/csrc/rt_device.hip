@@ -410,7 +410,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
 #endif
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
-  const bool vol = sc->hdr.has_volume != 0, tex = sc->hdr.has_textures != 0;
+  // VOL kernels: ConstantMedium nodes or an Isotropic material (also usable outside one)
+  const bool vol = (sc->hdr.has_volume | sc->hdr.has_isotropic) != 0;
+  const bool tex = sc->hdr.has_textures != 0;
   const bool bvh = sc->hdr.has_bvh != 0;
   typedef void (*kern_t)(TraceParams);
   // [count][vol][tex][bvh]; a scene without a BVH whose tables are staged in LDS runs the

@@ -513,7 +513,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   }
   // materials
   F.mats.assign(n_mat * RTL_MAT_WORDS, 0u);
-  bool pdf_mats = false, textured = false;
+  bool pdf_mats = false, textured = false, isotropic = false;
   for (uint64_t m = 0; m < n_mat; ++m) {
     uint64_t b = mat_off + m * RT_MAT_SLOTS;
     uint32_t* o = &F.mats[m * RTL_MAT_WORDS];
@@ -530,6 +530,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
         o[1] = (uint32_t)t;
         o[0] = (uint32_t)kind | (tex_needs_uv(F.texs, (uint32_t)t, 0) ? RTL_MATF_NEEDS_UV : 0u);
         if (kind != RT_MAT_DIFFUSE_LIGHT) pdf_mats = true;
+        if (kind == RT_MAT_ISOTROPIC) isotropic = true;
         if (F.texs[(size_t)t * RTL_TEX_WORDS] != RT_TEX_SOLID) textured = true;
         break;
       }
@@ -651,6 +652,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.n_texel_bytes = (uint32_t)n_texel;
   h.pdf_materials = pdf_mats;
   h.has_textures = textured;
+  h.has_isotropic = isotropic;
   return RT_OK;
 }
 

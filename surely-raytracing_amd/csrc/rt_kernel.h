@@ -1476,7 +1476,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // those of the separate branches.
     PROF(4);
     const bool diel = kind == RT_MAT_DIELECTRIC;
-    const bool iso = kind == RT_MAT_ISOTROPIC;
+    const bool iso = VOL && kind == RT_MAT_ISOTROPIC;  // VOL kernels: volumes or Isotropic
     C.inc(diel ? RT_OP_DIELECTRIC : (iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN));
     // unit(r_in.direction) (material.rs:170) or CosinePDF's w = unit(normal) (pdf.rs:58-62)
     const d3 uu = unit_vector(diel ? rd : normal);

@@ -125,4 +125,5 @@ typedef struct rtl_scene_header {
   uint32_t bvh_words;     /* BVH region: node words [0, bvh_words) hold every BVH record */
   uint32_t volume_in_bvh; /* a ConstantMedium lies inside a BVH subtree                */
   uint32_t volumes_one_walk_spheres; /* every ConstantMedium boundary is a one-walk sphere */
+  uint32_t has_isotropic; /* some material is Isotropic (also outside a ConstantMedium)  */
 } rtl_scene_header;

@@ -179,6 +179,23 @@ def test_bvh_over_instances_volumes_and_general_quads(gpu_available):
     _compare(blob, cam)
 
 
+def test_isotropic_material_outside_a_volume(gpu_available):
+    """Isotropic is an ordinary Material in the reference (material.rs:229-248): a sphere may use
+    it directly, with no ConstantMedium in the scene; the volume-capable kernel must run."""
+    sc = rt.Scene(4)
+    iso = sc.isotropic((0.8, 0.6, 0.4))
+    white = sc.lambertian((0.7, 0.7, 0.7))
+    light = sc.diffuse_light((8, 8, 8))
+    world = sc.hittable_list(sc.sphere((0, 1, 0), 1.0, iso),
+                             sc.quad((-4, 0, -4), (8, 0, 0), (0, 0, 8), white),
+                             sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 48, 9, 10, 40, (0, 2, 7), (0, 1, 0), (0, 1, 0), 0, 0, (0.1, 0.1, 0.1))
+    acc_g, _, st = _compare(blob, cam)
+    assert st.op_counts()["isotropic"] > 0
+
+
 def test_reference_semantics_flag(gpu_available):
     """RT_FLAG_SEMANTICS_REFERENCE: empty light list + diffuse material is an error, as the
     reference panics (hittable.rs:115-129 via render.rs:140-142)."""
