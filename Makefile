@@ -9,13 +9,14 @@ BUILD    := build
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 # device path is f64; contraction off, fma written explicitly (deterministic bits)
-HIPFLAGS := --offload-arch=$(ARCH) -Iinclude -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS := --offload-arch=$(ARCH) -Iinclude -I$(BUILD) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra
 CFLAGS_O := -std=c11 -O2 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
 HOST_SRC := $(CSRC)/host/scene.cpp $(CSRC)/host/presets.cpp $(CSRC)/host/capi.cpp
-DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp
-DEV_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp include/rt_mi355x.h
+DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp $(CSRC)/rt_jit.cpp
+DEV_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp $(CSRC)/rt_jit.hpp include/rt_mi355x.h $(BUILD)/rt_jit_sources.inc
+JIT_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_layout.h include/rt_mi355x.h $(CSRC)/rt_rng.h
 
 .PHONY: all device host oracle cli clean
 all: device host oracle cli
@@ -25,9 +26,14 @@ host: $(BUILD)/librthost.so
 cli: $(BUILD)/rt_render_cli
 oracle: oracle/_build/liboracle_f32.so oracle/_build/liboracle_f64.so
 
+# device headers embedded for the scene-specialised kernels compiled at run time (rt_jit.cpp)
+$(BUILD)/rt_jit_sources.inc: $(JIT_HDR) $(CSRC)/embed_sources.py
+	@mkdir -p $(BUILD)
+	python3 $(CSRC)/embed_sources.py $@ $(JIT_HDR)
+
 $(BUILD)/librtmi355x.so: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -shared $(DEV_SRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -shared $(DEV_SRC) -o $@ -lhiprtc
 
 $(BUILD)/librthost.so: $(HOST_SRC) $(CSRC)/host/scene.hpp include/rt_host.h include/rt_mi355x.h
 	@mkdir -p $(BUILD)
@@ -51,18 +57,18 @@ clean:
 VARIANTS := $(BUILD)/variants
 variants: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(VARIANTS)
-	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TRAV2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_trav2.so
-	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so
-	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TRAV2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_trav2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so -lhiprtc
 
 # occupancy variants of the BVH kernels; A/B with
 # VARDIR=build/variants_occ python tools_gpu/ab_variants.py W SPP ROUNDS SCENE
 variants-occ: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_occ
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=3 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh3.so
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=4 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh4.so
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=3 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh3.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=4 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh4.so -lhiprtc
 
 # section-cycle profiling build (tools_gpu/prof_sections.py); not shipped
 prof: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/prof
-	$(HIPCC) $(HIPFLAGS) -DRT_PROF -shared $(DEV_SRC) -o $(BUILD)/prof/librtmi355x.so
+	$(HIPCC) $(HIPFLAGS) -DRT_PROF -shared $(DEV_SRC) -o $(BUILD)/prof/librtmi355x.so -lhiprtc

@@ -178,6 +178,11 @@ def main():
     trace = ds.trace_ms(args.steps)
     kernel_ms = sum(trace) / max(1, len(trace))
 
+    # the product kernel that ran: scene-specialised (world walker generated from the scene,
+    # compiled by hiprtc at the first render, outside the timed region) or the interpreter
+    jstate, jmsg = ds.jit_info()
+    walker = ("scene-specialised (rt_jit.cpp, hiprtc)" if jstate == 1
+              else f"interpreter ({jmsg.splitlines()[0] if jmsg else 'jit state %d' % jstate})")
     if rank == 0:
         total = W * H * spp * args.steps
         value = total / elapsed / 1e6
@@ -199,6 +204,7 @@ def main():
                             f" ({args.config_name})",
                 "width": W, "height": H, "spp_effective": spp, "max_depth": cam.max_depth,
                 "seed": args.seed, "parallelism": f"cyclic rows x{world}, gather to rank 0",
+                "walker": walker,
             },
         }
         if ops is not None:

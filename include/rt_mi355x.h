@@ -133,6 +133,8 @@ typedef struct rt_camera {
 #define RT_FLAG_COUNT_OPS 0x2u             /* run the op-counting build, fill rt_stats.ops   */
 #define RT_FLAG_SEMANTICS_REFERENCE 0x4u   /* exact reference semantics: empty lights -> error, */
                                            /* Isotropic scattering_pdf = 0 */
+#define RT_FLAG_INTERPRETER 0x8u           /* product render with the interpreter walker, not the */
+                                           /* scene-specialised kernel (same image, bit for bit)  */
 
 typedef struct rt_render_opts {
   uint64_t seed;      /* render RNG seed                                   */
@@ -205,6 +207,17 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* scene);
 /* Bytes of the device-side flattened scene (nodes + materials + textures + tables). */
 uint64_t rt_scene_device_bytes(const rt_scene* scene);
+/* Scene-specialised product kernel (the world walker generated from the scene and compiled by
+ * hiprtc on the first product render; BVH / ConstantMedium scenes use the interpreter walkers).
+ * *state: 1 compiled and in use, 0 not compiled yet, -1 not generated for this scene (or
+ * RT_JIT=0), -2 compilation failed (the interpreter kernel runs). msg: the reason or the log. */
+int rt_scene_jit_info(rt_scene* scene, int* state, char* msg, uint32_t msg_len);
+/* Host-only check of the scene-specialised kernel (no device needed): generate the walker for
+ * `blob` and compile it with hiprtc for `arch` (e.g. "gfx950"). RT_OK with *state = 1 (compiled;
+ * msg receives the generated walker source) or -1 (not generated; msg says why); a negative
+ * status when compilation fails (msg receives the log). */
+int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* msg,
+                 uint32_t msg_len);
 
 /* Synchronous: render into a HOST buffer (n_rows * W * 3 floats). */
 int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts, float* accum_rgb,

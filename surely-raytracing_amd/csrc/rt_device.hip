@@ -30,6 +30,7 @@
 
 #include "rt_mi355x.h"
 #include "rt_flatten.hpp"
+#include "rt_jit.hpp"
 #include "rt_kernel.h"
 #include "rt_layout.h"
 
@@ -131,8 +132,14 @@ struct rt_scene {
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
-  int resident_blocks[40] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
-  size_t resident_lds[40] = {};  // ... at this dynamic LDS size
+  int resident_blocks[48] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
+  size_t resident_lds[48] = {};  // ... at this dynamic LDS size
+  // scene-specialised product kernel (rt_jit.cpp): the generated world walker, compiled on the
+  // first product render. jit_state: 0 = not compiled yet, 1 = compiled, -1 = scene not
+  // generated (jit_msg says why), -2 = compile failed (jit_msg = log; the interpreter runs)
+  std::string jit_walker, jit_msg;
+  int jit_state = -1;
+  rtj::Kernel jit_k[4];  // [tex][staged]
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -255,6 +262,13 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   sc->o_lights = (uint32_t)o_lig;
   sc->o_loffs = (uint32_t)o_loff;
   sc->o_perl = (uint32_t)o_perl;
+  const char* jit_env = std::getenv("RT_JIT");
+  if (jit_env && std::strcmp(jit_env, "0") == 0) {
+    sc->jit_msg = "disabled by RT_JIT=0";
+  } else {
+    sc->jit_walker = rtj::generate(F, &sc->jit_msg);
+    sc->jit_state = sc->jit_walker.empty() ? -1 : 0;
+  }
   sc->sphere_light0 = -1;
   for (size_t i = 0; i < F.light_offs.size(); ++i)
     if ((F.lights[F.light_offs[i]] & 0xffu) == RTL_SPHERE) {
@@ -280,6 +294,44 @@ void rt_scene_destroy(rt_scene* sc) {
 }
 
 uint64_t rt_scene_device_bytes(const rt_scene* sc) { return sc ? sc->dev_bytes : 0; }
+
+int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* msg,
+                 uint32_t msg_len) {
+  if (!blob || !arch || !state) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  rtf::FlatScene F;
+  std::string err;
+  int rc = rtf::flatten(blob, &F, &err);
+  if (rc != RT_OK) return set_err(rc, err);
+  std::string why, out;
+  const std::string walker = rtj::generate(F, &why);
+  *state = walker.empty() ? -1 : 1;
+  out = walker.empty() ? why : walker;
+  if (!walker.empty()) {
+    std::vector<char> code;
+    std::string log;
+    rc = rtj::compile(rtj::kernel_source(walker, F.hdr.has_textures != 0, true), arch, &code, &log);
+    if (rc != 0) {
+      *state = -2;
+      out = log;
+    }
+  }
+  if (msg && msg_len) {
+    std::strncpy(msg, out.c_str(), msg_len - 1);
+    msg[msg_len - 1] = '\0';
+  }
+  return *state == -2 ? set_err(RT_ERR_HIP, out) : RT_OK;
+}
+
+int rt_scene_jit_info(rt_scene* sc, int* state, char* msg, uint32_t msg_len) {
+  if (!sc || !state) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lock(sc->mu);
+  *state = sc->jit_state;
+  if (msg && msg_len) {
+    std::strncpy(msg, sc->jit_msg.c_str(), msg_len - 1);
+    msg[msg_len - 1] = '\0';
+  }
+  return RT_OK;
+}
 
 int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
                      float* accum, void* stream_v, rt_stats* stats) {
@@ -450,17 +502,36 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const bool novoli = novolb && sc->hdr.volumes_one_walk_spheres && !(opts->flags & RT_FLAG_COUNT_OPS);
   const int vb = (novoli ? 4 : 0) + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0);
   kern_t kern = staged ? table_staged[kidx / 2 - 8] : (novolb ? table_bvh_novolb[vb] : table[kidx]);
-  const int kslot = novolb ? 32 + vb : kidx;
+  int kslot = novolb ? 32 + vb : kidx;
+  // product renders of a generated scene run its scene-specialised kernel (same template
+  // arguments and launch bounds as `kern`, traversal unrolled; rt_jit.cpp)
+  hipFunction_t jfn = nullptr;
+  if (!count && !vol && !bvh && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
+      lds_bytes <= (64u << 10)) {
+    rtj::Kernel& jk = sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)];
+    if (!jk.fn) {
+      std::string log;
+      if (rtj::get_kernel(sc->jit_walker, sc->device, tex, staged, &jk, &log) != 0) {
+        sc->jit_state = -2;
+        sc->jit_msg = log;
+      }
+    }
+    if (jk.fn) {
+      sc->jit_state = 1;
+      jfn = jk.fn;
+      kslot = 40 + (tex ? 1 : 0) + (staged ? 2 : 0);
+    }
+  }
   const int block = bvh ? kBlockBvh : kBlock;
-  if (lds_bytes > (64u << 10))
+  if (lds_bytes > (64u << 10) && !jfn)
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_bytes));
   if (sc->resident_blocks[kslot] == 0 || sc->resident_lds[kslot] != lds_bytes) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, block, lds_bytes) !=
-            hipSuccess ||
-        nb <= 0)
-      nb = 1;
+    const hipError_t oe =
+        jfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jfn, block, lds_bytes)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, block, lds_bytes);
+    if (oe != hipSuccess || nb <= 0) nb = 1;
     sc->resident_blocks[kslot] = nb;
     sc->resident_lds[kslot] = lds_bytes;
   }
@@ -476,7 +547,13 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
     const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
+    if (jfn) {
+      void* args[] = {&P};
+      HIP_TRY(hipModuleLaunchKernel(jfn, (unsigned)blocks, 1, 1, (unsigned)block, 1, 1,
+                                    (unsigned)lds_bytes, stream, args, nullptr));
+    } else {
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sc->tev[ring][1], stream));
     sc->tev_render[ring] = sc->n_render;

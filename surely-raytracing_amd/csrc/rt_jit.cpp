@@ -1,0 +1,319 @@
+// rt_jit.cpp — scene-specialised path kernels (rt_jit.hpp).
+//
+// The interpreter (rt_kernel.h traverse<UNI=true>) walks the flattened scene at run time: a
+// scalar load of each record header, a scalar branch on its type, the record's constants in
+// SGPRs, and register copies wherever the node types' states join. Outside BVH subtrees that
+// node sequence does not depend on the ray (render.rs:264 -> hittable.rs:88-109 visits every
+// list child in order), so it is known when the scene is created. generate() writes it out as
+// straight-line code: the same arithmetic functions in the same order (aquad_test, quad_test,
+// sphere_test_v, translate_in, rotate_y_in), each record's constants as exact hex-float
+// literals, the rcp of the ray direction formed once per frame and axis, and the winner kept
+// as one packed (record, frame) code. Per-lane results are therefore bit-identical to the
+// interpreter's (tests/test_gpu_parity.py::test_jit_*), which remains the path for BVH and
+// ConstantMedium scenes and for the op-counting build.
+//
+// hiprtc compiles rt_kernel.h (embedded at build time, build/rt_jit_sources.inc) plus the
+// generated walker and an rt_trace wrapper with the same template arguments and launch bounds
+// as the ahead-of-time kernel (about a second per scene on the host); modules are cached per
+// (source, device) for the process.
+#include "rt_jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <utility>
+#include <vector>
+
+#include "rt_jit_sources.inc"  // kJitSrcNames[], kJitSrcText[], kJitSrcCount (Makefile)
+
+namespace rtj {
+namespace {
+
+// Largest scene the generator unrolls (primitive tests per world query) and the packed
+// (record + 1) | (frame + 1) << 16 winner code's range.
+constexpr size_t kMaxPrims = 512;
+constexpr size_t kMaxWords = 0xfffe;
+
+double word_double(const std::vector<uint32_t>& N, size_t w) {
+  const uint64_t bits = (uint64_t)N[w] | ((uint64_t)N[w + 1] << 32);
+  double d;
+  std::memcpy(&d, &bits, sizeof d);
+  return d;
+}
+// payload double k of the record at `rec` (rt_layout.h: doubles start at word 4)
+double pd(const std::vector<uint32_t>& N, size_t rec, int k) { return word_double(N, rec + 4 + 2 * k); }
+
+std::string lit(double v) {  // exact: hex-float literal of the same bits
+  char b[64];
+  std::snprintf(b, sizeof b, "(%a)", v);
+  return b;
+}
+std::string lit3(double x, double y, double z) {
+  return "mk(" + lit(x) + ", " + lit(y) + ", " + lit(z) + ")";
+}
+
+struct Gen {
+  const std::vector<uint32_t>& N;
+  std::ostringstream o;
+  bool rcp[3] = {false, false, false};  // rcp of d per axis formed in the current frame
+  size_t prims = 0;
+
+  explicit Gen(const std::vector<uint32_t>& n) : N(n) {}
+
+  void frame_changed() { rcp[0] = rcp[1] = rcp[2] = false; }
+  void need_rcp(int k) {
+    static const char* ax = "xyz";
+    if (!rcp[k]) {
+      o << "    r" << ax[k] << " = rcp_nr1(d." << ax[k] << ");\n";
+      rcp[k] = true;
+    }
+  }
+  // xform_in of the record at x (transform.rs:59, 86-107)
+  void xform(size_t x) {
+    if ((N[x] & 0xffu) == RTL_TRANSLATE) {
+      o << "    C.inc(RT_OP_TRANSLATE);\n    translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4))
+        << ", o);\n";
+    } else {
+      o << "    C.inc(RT_OP_ROTATE_Y);\n    rotate_y_in(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3))
+        << ", o, d);\n";
+    }
+    frame_changed();
+  }
+  uint32_t code(size_t rec, int frame) const {
+    return (uint32_t)(rec + 1) | ((uint32_t)(frame + 1) << 16);
+  }
+  // world_quad_test of the QUAD record at q (object.rs:453-490)
+  void quad(size_t q, int frame) {
+    const uint32_t axis = RTL_QUAD_AXIS(N[q]);
+    o << "    t = closest;\n";
+    if (axis) {
+      const int k = (int)axis - 1;
+      need_rcp(k);
+      o << "    h = aquad_test<COUNT, " << k << ">(AQuad{" << N[q] << "u, " << lit(pd(N, q, 0)) << ", "
+        << lit(pd(N, q, 1)) << ", " << lit(pd(N, q, 2)) << ", " << lit(pd(N, q, 3)) << ", "
+        << lit(pd(N, q, 4)) << "}, o, d, mk(rx, ry, rz), tmin, closest, t, C);\n";
+    } else {
+      o << "    h = quad_test<COUNT>(N + " << (q + RTL_QUAD_GEN) << "u, o, d, tmin, closest, t, C);\n";
+    }
+    o << "    closest = t;\n    code = h ? " << code(q, frame) << "u : code;\n";
+    ++prims;
+  }
+  // sphere_test of the SPHERE record at s (object.rs:107-112, 145-184)
+  void sphere(size_t s, int frame) {
+    o << "    t = closest;\n    {\n      d3 c = " << lit3(pd(N, s, 0), pd(N, s, 1), pd(N, s, 2)) << ";\n";
+    if (N[s] & RTL_SPHERE_MOVING)
+      o << "      c = vfma(tm, " << lit3(pd(N, s, 4), pd(N, s, 5), pd(N, s, 6)) << ", c);\n";
+    o << "      h = sphere_test_v<COUNT>(c, " << lit(pd(N, s, 3)) << ", o, d, tmin, closest, t, C);\n"
+      << "    }\n    closest = t;\n    code = h ? " << code(s, frame) << "u : code;\n";
+    ++prims;
+  }
+};
+
+}  // namespace
+
+std::string generate(const rtf::FlatScene& F, std::string* why) {
+  const std::vector<uint32_t>& N = F.nodes;
+  if (N.size() > kMaxWords) {
+    *why = "node array too large for the packed winner code";
+    return "";
+  }
+  if (F.hdr.has_bvh || F.hdr.has_volume || F.hdr.has_isotropic) {
+    *why = "BVH / ConstantMedium scene: interpreter walkers";
+    return "";
+  }
+  Gen G(N);
+  std::ostringstream& o = G.o;
+  o << "struct TravGen {\n"
+       "  template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>\n"
+       "  static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,\n"
+       "      double& t_out, uint32_t& hn, int& hf, Rng& g, Ctr<COUNT>& C) {\n"
+       "    const kptr N = (kptr)P.nodes;\n"
+       "    (void)N; (void)tm; (void)g;\n"
+       "    const double tmin = 0.0001;  // render.rs:267\n"
+       "    double closest = kInf, t = 0.0;\n"
+       "    double rx = 0.0, ry = 0.0, rz = 0.0;\n"
+       "    bool h = false;\n"
+       "    uint32_t code = 0u;  // (record + 1) | (frame + 1) << 16 of the closest hit\n"
+       "    d3 o = ro, d = rd;\n";
+  size_t node = F.hdr.root;
+  int frame = -1;
+  for (size_t guard = 0;; ++guard) {
+    if (node + 4 > N.size() || guard > N.size()) {
+      *why = "malformed node sequence";
+      return "";
+    }
+    const uint32_t h0 = N[node], ty = h0 & 0xffu;
+    o << "    // record " << node << "\n";
+    if (ty == RTL_QUAD) {
+      G.quad(node, frame);
+      node = N[node + 3];
+    } else if (ty == RTL_QUADS) {
+      const uint32_t cnt = h0 >> 8;
+      for (uint32_t k = 0; k < cnt; ++k) G.quad(node + 4 + (size_t)k * RTL_QUAD_WORDS, frame);
+      node = N[node + 1];
+    } else if (ty == RTL_SPHERE) {
+      G.sphere(node, frame);
+      node = N[node + 3];
+    } else if (ty == RTL_TRANSLATE || ty == RTL_ROTATE_Y) {
+      G.xform(node);
+      frame = (int)node;
+      node = N[node + 3];
+    } else if (ty == RTL_EXIT) {
+      // frame_ray: the parent frame's ray, recomputed from the world ray through its chain
+      frame = (int)N[node + 2];
+      o << "    o = ro;\n    d = rd;\n";
+      G.frame_changed();
+      if (frame >= 0) {
+        const uint32_t len = N[(size_t)frame + 2];
+        for (uint32_t k = 0; k < len && k < RTL_MAX_CHAIN; ++k) G.xform(N[(size_t)frame + 4 + k]);
+      }
+      node = N[node + 3];
+    } else if (ty == RTL_OTHER) {
+      node = N[node + 1];
+    } else if (ty == RTL_END) {
+      break;
+    } else {
+      *why = "record type " + std::to_string(ty) + " is not generated";
+      return "";
+    }
+    if (G.prims > kMaxPrims) {
+      *why = "more than " + std::to_string(kMaxPrims) + " primitive tests per world query";
+      return "";
+    }
+  }
+  o << "    t_out = closest;\n"
+       "    const bool hit = code != 0u;\n"
+       "    hn = hit ? (code & 0xffffu) - 1u : hn;\n"
+       "    hf = hit ? (int)(code >> 16) - 1 : hf;\n"
+       "    return hit;\n"
+       "  }\n"
+       "};\n";
+  return o.str();
+}
+
+std::string kernel_source(const std::string& walker, bool tex, bool staged) {
+  std::ostringstream src;
+  src << "#include \"rt_kernel.h\"\nnamespace rtk {\n"
+      << walker
+      << "}  // namespace rtk\nusing namespace rtk;\n"
+         "extern \"C\" __global__ __launch_bounds__(BlockOf<false>::value, "
+         "(MinWaves<false, "
+      << (tex ? "true" : "false") << ", false>::value)) void rt_trace_jit(TraceParams P) {\n"
+      << "  trace_body<false, false, " << (tex ? "true" : "false") << ", false, "
+      << (staged ? "true" : "false") << ", false, true, TravGen>(P);\n}\n";
+  return src.str();
+}
+
+int compile(const std::string& src, const std::string& arch, std::vector<char>* code,
+            std::string* log) {
+  // hiprtc provides the HIP device runtime and the fixed-width integer types itself: the
+  // headers' <hip/hip_runtime.h> and <stdint.h> resolve to these stubs
+  static const char* kStdint =
+      "#pragma once\ntypedef unsigned char uint8_t; typedef unsigned short uint16_t;\n"
+      "typedef unsigned int uint32_t; typedef unsigned long uint64_t; typedef signed char int8_t;\n"
+      "typedef short int16_t; typedef int int32_t; typedef long int64_t;\n";
+  std::vector<const char*> hs, hn;
+  for (int k = 0; k < kJitSrcCount; ++k) {
+    hs.push_back(kJitSrcText[k]);
+    hn.push_back(kJitSrcNames[k]);
+  }
+  hs.push_back(kStdint);
+  hn.push_back("stdint.h");
+  hs.push_back("#pragma once\n");
+  hn.push_back("hip/hip_runtime.h");
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_trace_jit.hip", (int)hs.size(), hs.data(),
+                          hn.data()) != HIPRTC_SUCCESS) {
+    *log = "hiprtcCreateProgram failed";
+    return RT_ERR_HIP;
+  }
+  const std::string off = "--offload-arch=" + arch;
+  // the ahead-of-time build's arithmetic flags (Makefile HIPFLAGS): contraction off, so every
+  // fma is the one written in rt_kernel.h and the generated walker computes the same bits
+  std::vector<const char*> opts = {off.c_str(), "-O3", "-std=c++17", "-ffp-contract=off",
+                                   "-fno-gpu-flush-denormals-to-zero"};
+  // build knobs of this library (ablation / occupancy variants, Makefile) apply to its
+  // run-time kernels too
+#define RTJ_STR2(x) #x
+#define RTJ_STR(x) RTJ_STR2(x)
+#ifdef RT_POOL_SI
+  opts.push_back("-DRT_POOL_SI=" RTJ_STR(RT_POOL_SI));
+#endif
+#ifdef RT_MIN_WAVES
+  opts.push_back("-DRT_MIN_WAVES=" RTJ_STR(RT_MIN_WAVES));
+#endif
+#ifdef RT_PROF
+  opts.push_back("-DRT_PROF");
+#endif
+#ifdef RT_ABL_TRAV2
+  opts.push_back("-DRT_ABL_TRAV2");
+#endif
+#ifdef RT_ABL_NOLPDF
+  opts.push_back("-DRT_ABL_NOLPDF");
+#endif
+#ifdef RT_ABL_LPDF2
+  opts.push_back("-DRT_ABL_LPDF2");
+#endif
+#ifdef RT_ABL_HIT2
+  opts.push_back("-DRT_ABL_HIT2");
+#endif
+#ifdef RT_ABL_SEED2
+  opts.push_back("-DRT_ABL_SEED2");
+#endif
+  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
+  size_t n = 0;
+  hiprtcGetProgramLogSize(prog, &n);
+  std::string plog(n, '\0');
+  if (n) hiprtcGetProgramLog(prog, &plog[0]);
+  if (rc != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    *log = "hiprtc: " + plog;
+    return RT_ERR_HIP;
+  }
+  size_t code_size = 0;
+  hiprtcGetCodeSize(prog, &code_size);
+  code->resize(code_size);
+  hiprtcGetCode(prog, code->data());
+  hiprtcDestroyProgram(&prog);
+  return 0;
+}
+
+int get_kernel(const std::string& walker, int device, bool tex, bool staged, Kernel* out,
+               std::string* log) {
+  static std::mutex mu;
+  static std::map<std::pair<int, std::string>, Kernel> cache;
+  const std::string s = kernel_source(walker, tex, staged);
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_pair(device, s);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    *out = it->second;
+    return 0;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    *log = "hipGetDeviceProperties failed";
+    return RT_ERR_HIP;
+  }
+  std::string arch = prop.gcnArchName;
+  const size_t colon = arch.find(':');  // "gfx950:sramecc+:xnack-" -> gfx950
+  if (colon != std::string::npos) arch.resize(colon);
+  std::vector<char> code;
+  const int rc = compile(s, arch, &code, log);
+  if (rc != 0) return rc;
+  Kernel k;
+  if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess ||
+      hipModuleGetFunction(&k.fn, k.mod, "rt_trace_jit") != hipSuccess) {
+    *log = "hipModuleLoadData / hipModuleGetFunction failed";
+    return RT_ERR_HIP;
+  }
+  cache.emplace(key, k);
+  *out = k;
+  return 0;
+}
+
+}  // namespace rtj

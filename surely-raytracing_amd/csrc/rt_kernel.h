@@ -451,14 +451,23 @@ __device__ __forceinline__ bool aquad_dispatch(const AQuad& q, Ptr Q, d3 o, d3 d
   }
 }
 
+template <bool COUNT>
+__device__ __forceinline__ bool sphere_test_v(d3 center, double r, d3 o, d3 d, double tmin,
+                                              double tmax, double& t_out, Ctr<COUNT>& C);
 // Sphere::hit object.rs:145-184; strict interval (Interval::surrounds interval.rs:25-27).
 template <bool COUNT, class Ptr>
 __device__ __forceinline__ bool sphere_test(Ptr s, d3 o, d3 d, double tm, double tmin,
                                             double tmax, double& t_out, Ctr<COUNT>& C) {
-  C.inc(RT_OP_SPHERE_TESTS);
   d3 center = ld3(s, 0);
-  double r = ldd(s, 3);
   if (s[0] & RTL_SPHERE_MOVING) center = vfma(tm, ld3(s, 4), center);  // Sphere::center(time) object.rs:107-112
+  return sphere_test_v<COUNT>(center, ldd(s, 3), o, d, tmin, tmax, t_out, C);
+}
+// sphere_test on a center (at the ray's time) and radius already in registers; the generated
+// scene walkers (rt_jit.cpp) pass them as literals.
+template <bool COUNT>
+__device__ __forceinline__ bool sphere_test_v(d3 center, double r, d3 o, d3 d, double tmin,
+                                              double tmax, double& t_out, Ctr<COUNT>& C) {
+  C.inc(RT_OP_SPHERE_TESTS);
   d3 oc = o - center;
   double a = dot(d, d);
   double half_b = dot(oc, d);
@@ -521,14 +530,17 @@ __device__ __forceinline__ bool aabb_hit_bf(const double (&mn)[3], const double 
 }
 
 // Translate/RotateY ray into object space (transform.rs:59, 86-107).
+__device__ __forceinline__ void translate_in(d3 off, d3& o) { o = o - off; }
+__device__ __forceinline__ void rotate_y_in(double s, double c, d3& o, d3& d) {
+  o = mk(fma(c, o.x, -(s * o.z)), o.y, fma(s, o.x, c * o.z));
+  d = mk(fma(c, d.x, -(s * d.z)), d.y, fma(s, d.x, c * d.z));
+}
 template <class Ptr>
 __device__ __forceinline__ void xform_in(Ptr X, d3& o, d3& d) {
   if ((X[0] & 0xffu) == RTL_TRANSLATE) {
-    o = o - ld3(X, 2);
+    translate_in(ld3(X, 2), o);
   } else {
-    double s = ldd(X, 2), c = ldd(X, 3);
-    o = mk(fma(c, o.x, -(s * o.z)), o.y, fma(s, o.x, c * o.z));
-    d = mk(fma(c, d.x, -(s * d.z)), d.y, fma(s, d.x, c * d.z));
+    rotate_y_in(ldd(X, 2), ldd(X, 3), o, d);
   }
 }
 // Hit record back to the parent space (transform.rs:65, 114-130).

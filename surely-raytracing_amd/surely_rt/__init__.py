@@ -34,6 +34,7 @@ RT_ERR_NO_DEVICE = -6
 RT_FLAG_OVERWRITE = 0x1
 RT_FLAG_COUNT_OPS = 0x2
 RT_FLAG_SEMANTICS_REFERENCE = 0x4
+RT_FLAG_INTERPRETER = 0x8  # product render with the interpreter walker (no scene-specialised kernel)
 
 OP_NAMES = [
     "samples", "world_queries", "quad_tests", "quad_plane", "quad_interval", "quad_hits",
@@ -187,6 +188,9 @@ def load_device_lib(path: Path) -> C.CDLL:
                                             C.c_int]),
         "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
                                         C.POINTER(C.c_int)]),
+        "rt_scene_jit_info": (C.c_int, [p, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
+        "rt_jit_check": (C.c_int, [C.POINTER(RtSceneBlob), C.c_char_p, C.POINTER(C.c_int),
+                                   C.c_char_p, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -450,6 +454,14 @@ class DeviceScene:
                                               C.byref(st) if st is not None else None))
         return st
 
+    def jit_info(self) -> tuple[int, str]:
+        """(state, message) of the scene-specialised kernel: 1 compiled and in use, 0 not compiled
+        yet, -1 not generated for this scene, -2 compilation failed (rt_scene_jit_info)."""
+        st = C.c_int(0)
+        buf = C.create_string_buffer(1 << 16)
+        _check_dev(self._lib.rt_scene_jit_info(self._h, C.byref(st), buf, len(buf)))
+        return st.value, buf.value.decode(errors="replace")
+
     def trace_ms(self, n: int) -> list[float]:
         """Device ms of the rt_trace kernel alone for the last n renders (oldest first)."""
         buf = (C.c_float * max(1, n))()
@@ -479,6 +491,15 @@ def layout_stats(blob: "Blob") -> dict:
     out = (C.c_uint32 * len(LAYOUT_STATS))()
     _check_dev(device_lib().rt_scene_layout_stats(blob.ref(), out, len(LAYOUT_STATS)))
     return dict(zip(LAYOUT_STATS, (int(v) for v in out)))
+
+
+def jit_check(blob: "Blob", arch: str = "gfx950") -> tuple[int, str]:
+    """Host-only: generate the scene-specialised walker for `blob` and compile it with hiprtc
+    (rt_jit_check). (1, walker source) | (-1, why not generated); raises on a compile error."""
+    st = C.c_int(0)
+    buf = C.create_string_buffer(1 << 20)
+    _check_dev(device_lib().rt_jit_check(blob.ref(), arch.encode(), C.byref(st), buf, len(buf)))
+    return st.value, buf.value.decode(errors="replace")
 
 
 def device_count() -> int:

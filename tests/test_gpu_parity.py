@@ -34,6 +34,11 @@ def _compare(blob, cam, seed=1, flags=rt.RT_FLAG_OVERWRITE, check_ops=True, **kw
     acc_p, _ = _gpu(blob, cam, seed=seed, flags=flags, **kw)
     assert np.array_equal(acc_p, acc_g, equal_nan=True), \
         f"product vs counting kernel: max |d| {np.nanmax(np.abs(acc_p - acc_g))}"
+    # scenes without BVH / ConstantMedium run a scene-specialised product kernel (rt_jit.cpp);
+    # the interpreter walker's product kernel must give the same image bit for bit
+    acc_i, _ = _gpu(blob, cam, seed=seed, flags=flags | rt.RT_FLAG_INTERPRETER, **kw)
+    assert np.array_equal(acc_p, acc_i, equal_nan=True), \
+        f"scene-specialised vs interpreter kernel: max |d| {np.nanmax(np.abs(acc_p - acc_i))}"
     opts = rt.make_opts(cam, seed=seed, flags=flags, **kw)
     acc_o, ops_o = O.render(blob, cam, opts, precision=64)
     spp = cam.samples_per_pixel
@@ -194,6 +199,56 @@ def test_isotropic_material_outside_a_volume(gpu_available):
     cam = rt.camera_new(1.0, 48, 9, 10, 40, (0, 2, 7), (0, 1, 0), (0, 1, 0), 0, 0, (0.1, 0.1, 0.1))
     acc_g, _, st = _compare(blob, cam)
     assert st.op_counts()["isotropic"] > 0
+
+
+def _jit_state(blob, cam):
+    ds = rt.DeviceScene(blob)
+    try:
+        ds.render(cam, rt.make_opts(cam))
+        return ds.jit_info()
+    finally:
+        ds.close()
+
+
+def test_jit_kernel_runs_for_cornell(gpu_available):
+    """BASELINE C2's scene renders through its scene-specialised kernel (compiled by hiprtc on
+    the first product render), not the interpreter."""
+    blob, cam = rt.preset_blob("cornell_box", width=48, spp=4)
+    state, msg = _jit_state(blob, cam)
+    assert state == 1, msg
+    blob, cam = rt.preset_blob("cornell_smoke", width=48, spp=4)
+    assert _jit_state(blob, cam)[0] == -1  # ConstantMedium: interpreter walkers
+
+
+def test_jit_general_quads_moving_spheres_nested_transforms(gpu_available):
+    """Every record kind the generator emits: general (non axis-aligned) quads, axis quads on
+    all three axes, moving spheres (time), nested Translate/RotateY chains with EXITs back to a
+    transformed parent frame, checker texture (TEX kernel), metal / dielectric / light."""
+    sc = rt.Scene(5)
+    chk = sc.lambertian(tex=sc.checker_from_color(0.7, (0.9, 0.2, 0.1), (0.1, 0.3, 0.9)))
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    glass = sc.dielectric(1.5)
+    metal = sc.metal((0.8, 0.7, 0.6), 0.2)
+    light = sc.diffuse_light((7, 7, 7))
+    inner = sc.hittable_list(sc.make_box((0, 0, 0), (0.8, 1.6, 0.8), white),
+                             sc.translate(sc.rotate_y(sc.sphere_moving((0.2, 2.0, 0.2), (0.4, 2.2, 0.1), 0.3, metal), 25), (0.1, 0.0, 0.3)))
+    nested = sc.translate(sc.rotate_y(inner, -18), (-1.2, 0, 0.4))
+    world = sc.hittable_list(
+        # ground off the checker's discontinuity plane y = 0 (see the mix test above)
+        sc.quad((-4, -0.3, -4), (8, 0, 0), (0, 0, 8), chk),
+        sc.quad((-3, 0.2, -2), (2.0, 1.0, 0.5), (0.3, 0.0, 1.5), white),  # general quad
+        nested,
+        sc.sphere((1.3, 0.7, 0.3), 0.7, glass),
+        sc.sphere_moving((1.5, 0.4, -1.5), (1.5, 0.9, -1.5), 0.4, white),
+        sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light),
+        sc.quad((3.5, 0.5, -1), (0, 2, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light),
+                              sc.sphere((1.3, 0.7, 0.3), 0.7, glass))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 72, 16, 30, 40, (0, 2.5, 8), (0, 1, 0), (0, 1, 0), 0, 0, (0.05, 0.05, 0.08))
+    state, msg = _jit_state(blob, cam)
+    assert state == 1, msg
+    _compare(blob, cam)
 
 
 def test_reference_semantics_flag(gpu_available):
