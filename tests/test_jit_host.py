@@ -41,9 +41,3 @@ def test_cornell_walker_sequence():
     assert all(struct.pack("<d", v) == struct.pack("<d", float.fromhex(v.hex())) for v in lits)
     # rcp of each axis formed once per frame: 3 in the world frame, 3 in the box frame
     assert len(re.findall(r"r[xyz] = rcp_nr1", src)) == 6
-
-
-def test_jit_check_rejects_bad_arch():
-    blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
-    with pytest.raises(rt.RtError):
-        rt.jit_check(blob, arch="gfx000")
