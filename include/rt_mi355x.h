@@ -208,7 +208,7 @@ void rt_scene_destroy(rt_scene* scene);
 /* Bytes of the device-side flattened scene (nodes + materials + textures + tables). */
 uint64_t rt_scene_device_bytes(const rt_scene* scene);
 /* Scene-specialised product kernel (the world walker generated from the scene and compiled by
- * hiprtc on the first product render; BVH / ConstantMedium scenes use the interpreter walkers).
+ * hiprtc on the first product render; BVH scenes use the interpreter walkers).
  * *state: 1 compiled and in use, 0 not compiled yet, -1 not generated for this scene (or
  * RT_JIT=0), -2 compilation failed (the interpreter kernel runs). msg: the reason or the log. */
 int rt_scene_jit_info(rt_scene* scene, int* state, char* msg, uint32_t msg_len);

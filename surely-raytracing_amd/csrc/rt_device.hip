@@ -309,7 +309,9 @@ int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* 
   if (!walker.empty()) {
     std::vector<char> code;
     std::string log;
-    rc = rtj::compile(rtj::kernel_source(walker, F.hdr.has_textures != 0, true), arch, &code, &log);
+    const bool vol = (F.hdr.has_volume | F.hdr.has_isotropic) != 0;
+    rc = rtj::compile(rtj::kernel_source(walker, vol, F.hdr.has_textures != 0, true), arch, &code,
+                      &log);
     if (rc != 0) {
       *state = -2;
       out = log;
@@ -506,12 +508,12 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   // product renders of a generated scene run its scene-specialised kernel (same template
   // arguments and launch bounds as `kern`, traversal unrolled; rt_jit.cpp)
   hipFunction_t jfn = nullptr;
-  if (!count && !vol && !bvh && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
+  if (!count && !bvh && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
       lds_bytes <= (64u << 10)) {
     rtj::Kernel& jk = sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)];
     if (!jk.fn) {
       std::string log;
-      if (rtj::get_kernel(sc->jit_walker, sc->device, tex, staged, &jk, &log) != 0) {
+      if (rtj::get_kernel(sc->jit_walker, sc->device, vol, tex, staged, &jk, &log) != 0) {
         sc->jit_state = -2;
         sc->jit_msg = log;
       }

@@ -9,8 +9,9 @@
 // sphere_test_v, translate_in, rotate_y_in), each record's constants as exact hex-float
 // literals, the rcp of the ray direction formed once per frame and axis, and the winner kept
 // as one packed (record, frame) code. Per-lane results are therefore bit-identical to the
-// interpreter's (tests/test_gpu_parity.py::test_jit_*), which remains the path for BVH and
-// ConstantMedium scenes and for the op-counting build.
+// interpreter's (tests/test_gpu_parity.py), which remains the path for BVH scenes and for the
+// op-counting build. A ConstantMedium record calls the interpreter's volume_hit (its boundary
+// walks stay interpreted).
 //
 // hiprtc compiles rt_kernel.h (embedded at build time, build/rt_jit_sources.inc) plus the
 // generated walker and an rt_trace wrapper with the same template arguments and launch bounds
@@ -121,8 +122,8 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
     *why = "node array too large for the packed winner code";
     return "";
   }
-  if (F.hdr.has_bvh || F.hdr.has_volume || F.hdr.has_isotropic) {
-    *why = "BVH / ConstantMedium scene: interpreter walkers";
+  if (F.hdr.has_bvh) {
+    *why = "BVH scene: interpreter walkers";
     return "";
   }
   Gen G(N);
@@ -172,6 +173,14 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
         for (uint32_t k = 0; k < len && k < RTL_MAX_CHAIN; ++k) G.xform(N[(size_t)frame + 4 + k]);
       }
       node = N[node + 3];
+    } else if (ty == RTL_VOLUME) {
+      // ConstantMedium (constant_medium.rs:41-95): the interpreter's boundary walks
+      o << "    h = volume_hit<COUNT, true, BVH, VOLI>(P, " << node << "u, make_uint4(" << N[node] << "u, "
+        << N[node + 1] << "u, " << N[node + 2] << "u, " << N[node + 3] << "u), ro, rd, tm, o, d, "
+        << frame << ", tmin, closest, t, g, C);\n"
+        << "    closest = h ? t : closest;\n    code = h ? " << G.code(node, frame) << "u : code;\n";
+      ++G.prims;
+      node = N[node + 1];
     } else if (ty == RTL_OTHER) {
       node = N[node + 1];
     } else if (ty == RTL_END) {
@@ -195,16 +204,18 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
   return o.str();
 }
 
-std::string kernel_source(const std::string& walker, bool tex, bool staged) {
+std::string kernel_source(const std::string& walker, bool vol, bool tex, bool staged) {
   std::ostringstream src;
   src << "#include \"rt_kernel.h\"\nnamespace rtk {\n"
       << walker
       << "}  // namespace rtk\nusing namespace rtk;\n"
          "extern \"C\" __global__ __launch_bounds__(BlockOf<false>::value, "
-         "(MinWaves<false, "
-      << (tex ? "true" : "false") << ", false>::value)) void rt_trace_jit(TraceParams P) {\n"
-      << "  trace_body<false, false, " << (tex ? "true" : "false") << ", false, "
-      << (staged ? "true" : "false") << ", false, true, TravGen>(P);\n}\n";
+         "(MinWaves<"
+      << (vol ? "true" : "false") << ", " << (tex ? "true" : "false")
+      << ", false>::value)) void rt_trace_jit(TraceParams P) {\n"
+      << "  trace_body<false, " << (vol ? "true" : "false") << ", " << (tex ? "true" : "false")
+      << ", false, " << (staged ? "true" : "false") << ", " << (vol ? "true" : "false")
+      << ", true, TravGen>(P);\n}\n";
   return src.str();
 }
 
@@ -282,11 +293,11 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   return 0;
 }
 
-int get_kernel(const std::string& walker, int device, bool tex, bool staged, Kernel* out,
-               std::string* log) {
+int get_kernel(const std::string& walker, int device, bool vol, bool tex, bool staged,
+               Kernel* out, std::string* log) {
   static std::mutex mu;
   static std::map<std::pair<int, std::string>, Kernel> cache;
-  const std::string s = kernel_source(walker, tex, staged);
+  const std::string s = kernel_source(walker, vol, tex, staged);
   std::lock_guard<std::mutex> lock(mu);
   auto key = std::make_pair(device, s);
   auto it = cache.find(key);

@@ -700,6 +700,76 @@ template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL, 
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
                          double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
+                         Ctr<COUNT>& C);
+// ConstantMedium::hit constant_medium.rs:41-95 for the VOLUME record at `node` (header h) in the
+// current frame (o, d): true when the free-flight distance ends inside the boundary before
+// `closest`, with the hit t in t_hit. Shared by the interpreter walker and the generated
+// walkers of rt_jit.cpp.
+template <bool COUNT, bool UNI, bool BVH, bool VOLI>
+__device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, uint4 h, d3 wo,
+                                           d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
+                                           double closest, double& t_hit, Rng& g, Ctr<COUNT>& C) {
+  typedef typename cond<UNI, kptr, gptr>::type Ptr;
+  const Ptr X = (Ptr)P.nodes + node;
+  C.inc(RT_OP_VOLUME_TESTS);
+  // rec1 = boundary.hit(r, (-inf, inf)), rec2 = boundary.hit(r, [rec1.t + 1e-4, inf)):
+  // one rolled loop, so the boundary walker is instantiated once
+  double t1 = 0.0, t2 = 0.0;
+  bool both = true;
+  const uint32_t fuse = h.x & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
+  if constexpr (UNI && !COUNT && !VOLI) {  // every boundary is a one-walk sphere
+    bool fb;
+    both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+  } else if (UNI && !COUNT && fuse) {
+    bool fb;
+    both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+    if (__ballot(fb) != 0ull) {  // rare: rerun the second query for those lanes
+      double tb;
+      uint32_t dn;
+      int df;
+      const bool b2 = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm, o, d,
+                                                              frame, t1 + 0.0001, kInf, tb,
+                                                              dn, df, g, C);
+      if (fb) {
+        both = b2;
+        t2 = tb;
+      }
+    }
+  } else {
+#pragma unroll 1
+    for (int pass = 0; pass < 2 && both; ++pass) {
+      double tb;
+      uint32_t dn;
+      int df;
+      both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
+                                                     o, d, frame,
+                                                     pass ? t1 + 0.0001 : -kInf, kInf,
+                                                     tb, dn, df, g, C);
+      if (pass) t2 = tb; else t1 = tb;
+    }
+  }
+  if (both) {
+    if (t1 < tmin) t1 = tmin;
+    if (t2 > closest) t2 = closest;
+    if (t1 < t2) {
+      if (t1 < 0.0) t1 = 0.0;
+      double ray_length = sqrt_nr(dot(d, d));
+      double dist_inside = (t2 - t1) * ray_length;
+      C.inc(RT_OP_VOLUME_DRAWS);
+      double hit_distance = ldd(X, 0) * log(rnd(g));
+      if (!(hit_distance > dist_inside)) {
+        t_hit = t1 + div_nr(hit_distance, ray_length);
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB, bool VOLI>
+__device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
+                         double tm, d3 o, d3 d, int frame, double tmin, double tmax,
+                         double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
                          Ctr<COUNT>& C) {
   typedef typename cond<UNI, kptr, gptr>::type Ptr;
   const Ptr N = (Ptr)P.nodes;
@@ -888,60 +958,13 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       if (!UNI) inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
       node = h.w;
     } else if (MAIN && VOL && type == RTL_VOLUME) {
-      // ConstantMedium::hit constant_medium.rs:41-95
-      C.inc(RT_OP_VOLUME_TESTS);
-      // rec1 = boundary.hit(r, (-inf, inf)), rec2 = boundary.hit(r, [rec1.t + 1e-4, inf)):
-      // one rolled loop, so the boundary walker is instantiated once
-      double t1 = 0.0, t2 = 0.0;
-      bool both = true;
-      const uint32_t fuse = h.x & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
-      if constexpr (UNI && !COUNT && !VOLI) {  // every boundary is a one-walk sphere
-        bool fb;
-        both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
-      } else if (UNI && !COUNT && fuse) {
-        bool fb;
-        both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
-        if (__ballot(fb) != 0ull) {  // rare: rerun the second query for those lanes
-          double tb;
-          uint32_t dn;
-          int df;
-          const bool b2 = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm, o, d,
-                                                                  frame, t1 + 0.0001, kInf, tb,
-                                                                  dn, df, g, C);
-          if (fb) {
-            both = b2;
-            t2 = tb;
-          }
-        }
-      } else {
-#pragma unroll 1
-        for (int pass = 0; pass < 2 && both; ++pass) {
-          double tb;
-          uint32_t dn;
-          int df;
-          both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
-                                                         o, d, frame,
-                                                         pass ? t1 + 0.0001 : -kInf, kInf,
-                                                         tb, dn, df, g, C);
-          if (pass) t2 = tb; else t1 = tb;
-        }
-      }
-      if (both) {
-        if (t1 < tmin) t1 = tmin;
-        if (t2 > closest) t2 = closest;
-        if (t1 < t2) {
-          if (t1 < 0.0) t1 = 0.0;
-          double ray_length = sqrt_nr(dot(d, d));
-          double dist_inside = (t2 - t1) * ray_length;
-          C.inc(RT_OP_VOLUME_DRAWS);
-          double hit_distance = ldd(X, 0) * log(rnd(g));
-          if (!(hit_distance > dist_inside)) {
-            closest = t1 + div_nr(hit_distance, ray_length);
-            hit = true;
-            hit_node = node;
-            hit_frame = frame;
-          }
-        }
+      double tv;
+      if (volume_hit<COUNT, UNI, BVH, VOLI>(P, node, h, wo, wd, tm, o, d, frame, tmin, closest, tv,
+                                            g, C)) {
+        closest = tv;
+        hit = true;
+        hit_node = node;
+        hit_frame = frame;
       }
       node = h.y;
     } else if (type == RTL_DUP) {

@@ -211,13 +211,15 @@ def _jit_state(blob, cam):
 
 
 def test_jit_kernel_runs_for_cornell(gpu_available):
-    """BASELINE C2's scene renders through its scene-specialised kernel (compiled by hiprtc on
-    the first product render), not the interpreter."""
+    """BASELINE C2's and C3's scenes render through their scene-specialised kernels (compiled by
+    hiprtc on the first product render), not the interpreter."""
     blob, cam = rt.preset_blob("cornell_box", width=48, spp=4)
     state, msg = _jit_state(blob, cam)
     assert state == 1, msg
     blob, cam = rt.preset_blob("cornell_smoke", width=48, spp=4)
-    assert _jit_state(blob, cam)[0] == -1  # ConstantMedium: interpreter walkers
+    assert _jit_state(blob, cam)[0] == 1  # ConstantMedium records call volume_hit
+    blob, cam = rt.preset_blob("final_scene", width=32, spp=1, depth=4)
+    assert _jit_state(blob, cam)[0] == -1  # BVH: interpreter walkers
 
 
 def test_jit_general_quads_moving_spheres_nested_transforms(gpu_available):
