@@ -268,6 +268,8 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   } else {
     sc->jit_walker = rtj::generate(F, &sc->jit_msg);
     sc->jit_state = sc->jit_walker.empty() ? -1 : 0;
+    if (sc->jit_state == 0 && F.hdr.has_bvh)
+      sc->jit_msg = "BVH scene: interpreter kernel (RT_JIT_BVH=1 opts in to the generated walker)";
   }
   sc->sphere_light0 = -1;
   for (size_t i = 0; i < F.light_offs.size(); ++i)
@@ -309,9 +311,7 @@ int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* 
   if (!walker.empty()) {
     std::vector<char> code;
     std::string log;
-    const bool vol = (F.hdr.has_volume | F.hdr.has_isotropic) != 0;
-    rc = rtj::compile(rtj::kernel_source(walker, vol, F.hdr.has_textures != 0, true), arch, &code,
-                      &log);
+    rc = rtj::compile(rtj::kernel_source(walker, rtj::product_flags(F, true)), arch, &code, &log);
     if (rc != 0) {
       *state = -2;
       out = log;
@@ -420,7 +420,13 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     P.bvh_lds_words = P.bvh_words;
     P.bvh_lds_off = 0;
   } else if (sc->hdr.has_bvh) {
-    const size_t room = kLdsBvhMax > P.stage_bytes ? kLdsBvhMax - P.stage_bytes : 0;
+    // a scene-specialised kernel (module launch) is given at most 64 KiB of dynamic LDS (the
+    // ahead-of-time kernels take hipFuncSetAttribute's opt-in for more)
+    const char* jb = std::getenv("RT_JIT_BVH");
+    const bool jit_lds = !(opts->flags & (RT_FLAG_COUNT_OPS | RT_FLAG_INTERPRETER)) &&
+                         sc->jit_state >= 0 && jb && std::strcmp(jb, "1") == 0;
+    const size_t cap = jit_lds ? std::min<size_t>(kLdsBvhMax, 64u << 10) : kLdsBvhMax;
+    const size_t room = cap > P.stage_bytes ? cap - P.stage_bytes : 0;
     P.bvh_lds_words = (uint32_t)std::min<size_t>(P.bvh_words, room / 64 * 16);
     P.bvh_lds_off = P.stage_bytes;
   }
@@ -506,14 +512,29 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   kern_t kern = staged ? table_staged[kidx / 2 - 8] : (novolb ? table_bvh_novolb[vb] : table[kidx]);
   int kslot = novolb ? 32 + vb : kidx;
   // product renders of a generated scene run its scene-specialised kernel (same template
-  // arguments and launch bounds as `kern`, traversal unrolled; rt_jit.cpp)
+  // arguments and launch bounds as `kern`, top-level walk unrolled; rt_jit.cpp)
   hipFunction_t jfn = nullptr;
-  if (!count && !bvh && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
-      lds_bytes <= (64u << 10)) {
+  // BVH scenes: the generated walker (BVH subtrees call the per-lane walker) compiles, but on
+  // this ROCm the queue aborts its 768-thread module launch (HSA_STATUS_ERROR_INVALID_ISA, while
+  // the same template's ahead-of-time kernel runs), so it is opt-in (RT_JIT_BVH=1) until that is
+  // understood
+  static const bool jit_bvh = [] {
+    const char* e = std::getenv("RT_JIT_BVH");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  if (!count && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
+      lds_bytes <= (64u << 10) && (!bvh || jit_bvh)) {
     rtj::Kernel& jk = sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)];
     if (!jk.fn) {
       std::string log;
-      if (rtj::get_kernel(sc->jit_walker, sc->device, vol, tex, staged, &jk, &log) != 0) {
+      rtj::Flags jf;
+      jf.vol = vol;
+      jf.tex = tex;
+      jf.bvh = bvh;
+      jf.staged = staged;
+      jf.volb = novolb ? false : vol;
+      jf.voli = !novoli;
+      if (rtj::get_kernel(sc->jit_walker, sc->device, jf, &jk, &log) != 0) {
         sc->jit_state = -2;
         sc->jit_msg = log;
       }
@@ -525,7 +546,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     }
   }
   const int block = bvh ? kBlockBvh : kBlock;
-  if (lds_bytes > (64u << 10) && !jfn)
+  // (module kernels take their dynamic LDS size at launch; `kern` also serves as the fallback
+  // should a scene-specialised launch be refused)
+  if (lds_bytes > (64u << 10))
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_bytes));
   if (sc->resident_blocks[kslot] == 0 || sc->resident_lds[kslot] != lds_bytes) {
@@ -551,8 +574,16 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
     if (jfn) {
       void* args[] = {&P};
-      HIP_TRY(hipModuleLaunchKernel(jfn, (unsigned)blocks, 1, 1, (unsigned)block, 1, 1,
-                                    (unsigned)lds_bytes, stream, args, nullptr));
+      const hipError_t le = hipModuleLaunchKernel(jfn, (unsigned)blocks, 1, 1, (unsigned)block, 1,
+                                                  1, (unsigned)lds_bytes, stream, args, nullptr);
+      if (le != hipSuccess) {  // refused at launch (nothing ran): the interpreter kernel renders
+        (void)hipGetLastError();
+        sc->jit_state = -2;
+        sc->jit_msg = std::string("hipModuleLaunchKernel: ") + hipGetErrorString(le);
+        sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)] = rtj::Kernel{};
+        jfn = nullptr;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
+      }
     } else {
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
     }

@@ -9,9 +9,11 @@
 // sphere_test_v, translate_in, rotate_y_in), each record's constants as exact hex-float
 // literals, the rcp of the ray direction formed once per frame and axis, and the winner kept
 // as one packed (record, frame) code. Per-lane results are therefore bit-identical to the
-// interpreter's (tests/test_gpu_parity.py), which remains the path for BVH scenes and for the
-// op-counting build. A ConstantMedium record calls the interpreter's volume_hit (its boundary
-// walks stay interpreted).
+// interpreter's (tests/test_gpu_parity.py), which remains the op-counting build's path. A
+// ConstantMedium record calls the interpreter's volume_hit (its boundary walks stay
+// interpreted), and a BVH subtree record calls the interpreter's per-lane walker (traverse<UNI =
+// false>, hittable.rs:216-236) with the generated walk's closest hit, exactly as the UNI
+// interpreter hands the subtree over.
 //
 // hiprtc compiles rt_kernel.h (embedded at build time, build/rt_jit_sources.inc) plus the
 // generated walker and an rt_trace wrapper with the same template arguments and launch bounds
@@ -22,6 +24,7 @@
 #include <hip/hiprtc.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -34,10 +37,13 @@
 namespace rtj {
 namespace {
 
-// Largest scene the generator unrolls (primitive tests per world query) and the packed
-// (record + 1) | (frame + 1) << 16 winner code's range.
+// Largest scene the generator unrolls (primitive tests per world query) and the packed winner
+// code's range: (record + 1) | frame_id << 24, frame_id = the frame's ordinal in the walk (0 = the
+// world frame); kBvhCode marks "the last hit came from a BVH subtree" (record/frame in bhn/bhf).
 constexpr size_t kMaxPrims = 512;
-constexpr size_t kMaxWords = 0xfffe;
+constexpr size_t kMaxWords = 0xfffffe;
+constexpr size_t kMaxFrames = 254;
+constexpr uint32_t kBvhCode = 0xffffffffu;
 
 double word_double(const std::vector<uint32_t>& N, size_t w) {
   const uint64_t bits = (uint64_t)N[w] | ((uint64_t)N[w + 1] << 32);
@@ -62,6 +68,8 @@ struct Gen {
   std::ostringstream o;
   bool rcp[3] = {false, false, false};  // rcp of d per axis formed in the current frame
   size_t prims = 0;
+  std::vector<int> frames{-1};  // frame_id -> frame record (-1 = world)
+  bool bvh = false;             // a BVH subtree call was emitted
 
   explicit Gen(const std::vector<uint32_t>& n) : N(n) {}
 
@@ -84,8 +92,11 @@ struct Gen {
     }
     frame_changed();
   }
-  uint32_t code(size_t rec, int frame) const {
-    return (uint32_t)(rec + 1) | ((uint32_t)(frame + 1) << 16);
+  uint32_t code(size_t rec, int frame) {
+    size_t id = 0;
+    while (id < frames.size() && frames[id] != frame) ++id;
+    if (id == frames.size()) frames.push_back(frame);
+    return (uint32_t)(rec + 1) | ((uint32_t)id << 24);
   }
   // world_quad_test of the QUAD record at q (object.rs:453-490)
   void quad(size_t q, int frame) {
@@ -122,10 +133,6 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
     *why = "node array too large for the packed winner code";
     return "";
   }
-  if (F.hdr.has_bvh) {
-    *why = "BVH scene: interpreter walkers";
-    return "";
-  }
   Gen G(N);
   std::ostringstream& o = G.o;
   o << "struct TravGen {\n"
@@ -138,7 +145,9 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
        "    double closest = kInf, t = 0.0;\n"
        "    double rx = 0.0, ry = 0.0, rz = 0.0;\n"
        "    bool h = false;\n"
-       "    uint32_t code = 0u;  // (record + 1) | (frame + 1) << 16 of the closest hit\n"
+       "    uint32_t code = 0u;  // (record + 1) | frame_id << 24 of the closest hit\n"
+       "    uint32_t bhn = 0u;   // BVH subtree winner (code == kBvhCode)\n"
+       "    int bhf = -1;\n"
        "    d3 o = ro, d = rd;\n";
   size_t node = F.hdr.root;
   int frame = -1;
@@ -181,6 +190,19 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
         << "    closest = h ? t : closest;\n    code = h ? " << G.code(node, frame) << "u : code;\n";
       ++G.prims;
       node = N[node + 1];
+    } else if (ty == RTL_BVH) {
+      // BvhNode subtree [node, skip) per lane (rt_kernel.h traverse<UNI> RTL_BVH)
+      o << "    if (BVH) {\n      double tb;\n      uint32_t bn = 0u;\n      int bf = -1;\n"
+        << "      const bool sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, "
+        << N[node + 1] << "u, ro, rd, tm, o, d, " << frame
+        << ", tmin, closest, tb, bn, bf, g, C);\n"
+        << "      closest = sub ? tb : closest;\n      code = sub ? " << kBvhCode << "u : code;\n"
+        << "      bhn = sub ? bn : bhn;\n      bhf = sub ? bf : bhf;\n    }\n";
+      G.bvh = true;
+      ++G.prims;
+      node = N[node + 1];
+    } else if (ty == RTL_DUP) {
+      node = N[node + 1];
     } else if (ty == RTL_OTHER) {
       node = N[node + 1];
     } else if (ty == RTL_END) {
@@ -193,29 +215,55 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
       *why = "more than " + std::to_string(kMaxPrims) + " primitive tests per world query";
       return "";
     }
+    if (G.frames.size() > kMaxFrames) {
+      *why = "more than " + std::to_string(kMaxFrames) + " instance frames";
+      return "";
+    }
   }
   o << "    t_out = closest;\n"
        "    const bool hit = code != 0u;\n"
-       "    hn = hit ? (code & 0xffffu) - 1u : hn;\n"
-       "    hf = hit ? (int)(code >> 16) - 1 : hf;\n"
+       "    uint32_t rn = (code & 0xffffffu) - 1u;\n"
+       "    const uint32_t fid = code >> 24;\n"
+       "    int fr = -1;\n";
+  for (size_t id = 1; id < G.frames.size(); ++id)
+    o << "    fr = fid == " << id << "u ? " << G.frames[id] << " : fr;\n";
+  if (G.bvh)
+    o << "    rn = code == " << kBvhCode << "u ? bhn : rn;\n"
+      << "    fr = code == " << kBvhCode << "u ? bhf : fr;\n";
+  o << "    hn = hit ? rn : hn;\n"
+       "    hf = hit ? fr : hf;\n"
        "    return hit;\n"
        "  }\n"
        "};\n";
   return o.str();
 }
 
-std::string kernel_source(const std::string& walker, bool vol, bool tex, bool staged) {
+Flags product_flags(const rtf::FlatScene& F, bool staged) {
+  Flags f;
+  f.vol = (F.hdr.has_volume | F.hdr.has_isotropic) != 0;
+  f.tex = F.hdr.has_textures != 0;
+  f.bvh = F.hdr.has_bvh != 0;
+  f.staged = staged && !f.bvh;
+  // rt_device.hip: BVH scenes whose volumes all sit outside BVH subtrees run the per-lane walker
+  // without its volume branch, and without the two-walk interpreter when every boundary is a
+  // one-walk sphere
+  const bool novolb = f.bvh && f.vol && !F.hdr.volume_in_bvh;
+  f.volb = novolb ? false : f.vol;
+  f.voli = !(novolb && F.hdr.volumes_one_walk_spheres);
+  return f;
+}
+
+std::string kernel_source(const std::string& walker, const Flags& f) {
+  auto b = [](bool v) { return v ? "true" : "false"; };
   std::ostringstream src;
   src << "#include \"rt_kernel.h\"\nnamespace rtk {\n"
       << walker
       << "}  // namespace rtk\nusing namespace rtk;\n"
-         "extern \"C\" __global__ __launch_bounds__(BlockOf<false>::value, "
-         "(MinWaves<"
-      << (vol ? "true" : "false") << ", " << (tex ? "true" : "false")
-      << ", false>::value)) void rt_trace_jit(TraceParams P) {\n"
-      << "  trace_body<false, " << (vol ? "true" : "false") << ", " << (tex ? "true" : "false")
-      << ", false, " << (staged ? "true" : "false") << ", " << (vol ? "true" : "false")
-      << ", true, TravGen>(P);\n}\n";
+         "extern \"C\" __global__ __launch_bounds__(BlockOf<" << b(f.bvh) << ">::value, "
+         "(MinWaves<" << b(f.vol) << ", " << b(f.tex) << ", " << b(f.bvh)
+      << ">::value)) void rt_trace_jit(TraceParams P) {\n"
+      << "  trace_body<false, " << b(f.vol) << ", " << b(f.tex) << ", " << b(f.bvh) << ", "
+      << b(f.staged) << ", " << b(f.volb) << ", " << b(f.voli) << ", TravGen>(P);\n}\n";
   return src.str();
 }
 
@@ -290,14 +338,20 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   code->resize(code_size);
   hiprtcGetCode(prog, code->data());
   hiprtcDestroyProgram(&prog);
+  if (const char* dump = std::getenv("RT_JIT_DUMP")) {  // diagnostics: the code object as built
+    if (FILE* f = std::fopen(dump, "wb")) {
+      std::fwrite(code->data(), 1, code->size(), f);
+      std::fclose(f);
+    }
+  }
   return 0;
 }
 
-int get_kernel(const std::string& walker, int device, bool vol, bool tex, bool staged,
-               Kernel* out, std::string* log) {
+int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
+               std::string* log) {
   static std::mutex mu;
   static std::map<std::pair<int, std::string>, Kernel> cache;
-  const std::string s = kernel_source(walker, vol, tex, staged);
+  const std::string s = kernel_source(walker, f);
   std::lock_guard<std::mutex> lock(mu);
   auto key = std::make_pair(device, s);
   auto it = cache.find(key);

@@ -12,9 +12,18 @@ namespace rtj {
 
 // Source of `struct TravGen` (the world query of ray_color, render.rs:264-267) for this scene:
 // the wave-uniform node sequence that the interpreter (rt_kernel.h traverse<UNI>) walks at run
-// time, unrolled, with every record's constants as literals. Empty when the scene has records
-// the generator does not emit (BVH subtrees) or is too large; *why says which.
+// time, unrolled, with every record's constants as literals; a BVH subtree record becomes a call
+// of the interpreter's per-lane walker. Empty when the scene has records the generator does not
+// emit or is too large; *why says which.
 std::string generate(const rtf::FlatScene& F, std::string* why);
+
+// Template arguments of the path kernel (rt_kernel.h trace_body) the generated walker runs in;
+// the same as the ahead-of-time interpreter kernel the scene would otherwise launch.
+struct Flags {
+  bool vol = false, tex = false, staged = false, bvh = false, volb = false, voli = true;
+};
+// Flags of the product kernel for scene header `hdr` (rt_device.hip's kernel choice).
+Flags product_flags(const rtf::FlatScene& F, bool staged);
 
 // Kernel for (generated walker, feature flags) on `device`, compiled on first use and cached for
 // the process. Returns 0 or a negative rt status with *log filled.
@@ -22,12 +31,12 @@ struct Kernel {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
 };
-int get_kernel(const std::string& walker, int device, bool vol, bool tex, bool staged,
-               Kernel* out, std::string* log);
+int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
+               std::string* log);
 
 // The hiprtc translation unit (embedded headers + walker + rt_trace_jit wrapper) and its
 // compilation for `arch` (e.g. "gfx950") into a code object; host-only, no device needed.
-std::string kernel_source(const std::string& walker, bool vol, bool tex, bool staged);
+std::string kernel_source(const std::string& walker, const Flags& f);
 int compile(const std::string& src, const std::string& arch, std::vector<char>* code,
             std::string* log);
 

@@ -1,5 +1,6 @@
 """Scene-specialised kernels (rt_jit.cpp) on the host: the generator emits a walker for every
-scene without BVH records, hiprtc compiles it for gfx950 (no device needed),
+preset scene (BVH subtrees become calls of the per-lane walker), hiprtc compiles it for gfx950
+(no device needed),
 and the walker visits the records in the interpreter's order with the records' exact constants."""
 import re
 import struct
@@ -16,12 +17,27 @@ PRESETS = ["cornell_box", "cornell_smoke", "final_scene", "quads", "simple_light
 def test_generated_walker_compiles(name):
     blob, cam = rt.preset_blob(name, width=32, spp=4)
     state, msg = rt.jit_check(blob)
-    stats = rt.layout_stats(blob)
-    if stats["bvh_records"]:
-        assert state == -1 and msg
-    else:
-        assert state == 1, msg
-        assert "struct TravGen" in msg
+    assert state == 1, msg
+    assert "struct TravGen" in msg
+    # a BVH subtree record hands its [root, skip) range to the per-lane walker
+    n_calls = len(re.findall(r"traverse<true, COUNT, VOLB, false, BVH>", msg))
+    assert (n_calls > 0) == (rt.layout_stats(blob)["bvh_records"] > 0)
+
+
+def test_final_scene_walker_bvh_calls():
+    """final_scene (main.rs:603-709): the ground-box BVH at the world frame, the light quad, and
+    the sphere-cluster BVH inside Translate(RotateY(...)) with that instance frame."""
+    blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1, src
+    calls = re.findall(r"traverse<true, COUNT, VOLB, false, BVH>\(P, (\d+)u, (\d+)u, ro, rd, tm, o, d, "
+                       r"(-?\d+),", src)
+    assert len(calls) == 2
+    assert calls[0][2] == "-1" and calls[1][2] != "-1"
+    # the subtree's skip is the record the generated walk continues with
+    for root, skip, _ in calls:
+        assert int(skip) > int(root)
+    assert src.index("translate_in") < src.index("rotate_y_in") < src.index(f"P, {calls[1][0]}u")
 
 
 def test_cornell_walker_sequence():
