@@ -125,6 +125,93 @@ struct Gen {
   }
 };
 
+// The light-list PDF value of the mixture (rt_kernel.h light_pdf: HittableList::pdf_value
+// hittable.rs:115-124 over Quad/Sphere::pdf_value object.rs:492-501, 190-202), the list unrolled
+// with each light's constants as literals: the same expressions in the same order.
+bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string* why) {
+  const std::vector<uint32_t>& L = F.lights;
+  o << "  template <bool COUNT>\n"
+       "  static __device__ __forceinline__ double lights_pdf(const TraceParams& P, d3 origin, d3 dir,\n"
+       "      double cos_sl0, Ctr<COUNT>& C) {\n"
+       "    (void)P; (void)origin; (void)dir; (void)cos_sl0;\n"
+       "    double sum = 0.0, pv = 0.0;\n";
+  int sphere0 = -1;  // rt_device.hip sphere_light0: the first sphere light
+  for (size_t i = 0; i < F.light_offs.size(); ++i)
+    if ((L[F.light_offs[i]] & 0xffu) == RTL_SPHERE) {
+      sphere0 = (int)i;
+      break;
+    }
+  const size_t n = F.hdr.n_lights;  // the interpreter's P.n_lights
+  if (n > F.light_offs.size()) {
+    *why = "malformed light table";
+    return false;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const size_t off = F.light_offs[i];
+    if (off + 4 > L.size()) {
+      *why = "malformed light table";
+      return false;
+    }
+    const uint32_t type = L[off] & 0xffu;
+    o << "    // light " << i << "\n    pv = 0.0;\n";
+    if (type == RTL_QUAD) {
+      o << "    {\n      C.inc(RT_OP_LIGHT_PDF_QUAD);\n      double t = 0.0;\n      bool hq;\n";
+      const uint32_t axis = RTL_QUAD_AXIS(L[off]);
+      if (axis) {
+        const int k = (int)axis - 1;
+        const char* r[3] = {"0.", "0.", "0."};
+        const char* rc[3] = {"rcp_nr1(dir.x)", "rcp_nr1(dir.y)", "rcp_nr1(dir.z)"};
+        r[k] = rc[k];
+        o << "      hq = aquad_test<COUNT, " << k << ">(AQuad{" << L[off] << "u";
+        for (int j = 0; j < 5; ++j) o << ", " << lit(pd(L, off, RTL_LQUAD_AXIS_D + j));
+        o << "}, origin, dir, mk(" << r[0] << ", " << r[1] << ", " << r[2]
+          << "), 0.001, kInf, t, C);\n";
+      } else {
+        o << "      hq = quad_test<COUNT>((kptr)P.lights + " << off
+          << "u, origin, dir, 0.001, kInf, t, C);\n";
+      }
+      o << "      const double len2 = dot(dir, dir);\n"
+           "      const double dist2 = (t * t) * len2;\n"
+           "      const double cosine = fabs(dot(dir, "
+        << lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2))
+        << ")) * rsq_nr(len2);\n"
+           "      const double q = dist2 * rcp_w(cosine * "
+        << lit(pd(L, off, 7)) << ");\n      pv = hq ? q : 0.0;\n    }\n";
+    } else if (type == RTL_SPHERE) {
+      const std::string c = lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2));
+      const std::string r = lit(pd(L, off, 3));
+      o << "    {\n      C.inc(RT_OP_LIGHT_PDF_SPHERE);\n      bool hs;\n"
+           "      if (COUNT) {\n        double t = 0.0;\n"
+           "        hs = sphere_test<COUNT>((kptr)P.lights + " << off
+        << "u, origin, dir, 0.0, 0.001, kInf, t, C);\n      } else {\n"
+           "        const d3 oc = origin - " << c << ";\n"
+           "        const double a = dot(dir, dir);\n"
+           "        const double half_b = dot(oc, dir);\n"
+           "        const double r = " << r << ";\n"
+           "        const double c = dot(oc, oc) - r * r;\n"
+           "        const double disc = fma(half_b, half_b, -(a * c));\n"
+           "        const double c1 = fma(0.001, a, half_b);\n"
+           "        hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));\n      }\n"
+           "      double cos_max = 0.0;\n";
+      if ((int)i == sphere0) {
+        o << "      cos_max = cos_sl0;\n";
+      } else {
+        o << "      if (hs) {\n        d3 cmo = " << c << " - origin;\n        double r = " << r
+          << ";\n        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));\n      }\n";
+      }
+      o << "      const double solid = 2.0 * kPi * (1.0 - cos_max);\n"
+           "      const double q = rcp_w(solid);\n      pv = hs ? q : 0.0;\n    }\n";
+    }
+    o << (i == 0 ? "    sum = pv;\n" : "    sum = sum + pv;\n");
+  }
+  if (F.hdr.lights_is_list && n) {
+    o << "    return sum * " << lit(1.0 / (double)n) << ";\n  }\n";
+  } else {
+    o << "    return sum;\n  }\n";
+  }
+  return true;
+}
+
 }  // namespace
 
 std::string generate(const rtf::FlatScene& F, std::string* why) {
@@ -233,8 +320,9 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
   o << "    hn = hit ? rn : hn;\n"
        "    hf = hit ? fr : hf;\n"
        "    return hit;\n"
-       "  }\n"
-       "};\n";
+       "  }\n";
+  if (!gen_lights_pdf(F, o, why)) return "";
+  o << "};\n";
   return o.str();
 }
 

@@ -1217,6 +1217,12 @@ struct TravInterp {
     return traverse<true, COUNT, VOL, true, BVH, VOLB, VOLI>(P, P.root, ~0u, ro, rd, tm, ro, rd,
                                                              -1, 0.0001, kInf, t, hn, hf, g, C);
   }
+  // the mixture's light-list PDF value (pdf.rs:91-93)
+  template <bool COUNT>
+  static __device__ __forceinline__ double lights_pdf(const TraceParams& P, d3 origin, d3 dir,
+                                                      double cos_sl0, Ctr<COUNT>& C) {
+    return light_pdf<COUNT>(P, origin, dir, cos_sl0, C);
+  }
 };
 
 // The path kernel body; instantiated by rt_device.hip (interpreter) and by scene-specialised
@@ -1613,7 +1619,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       double pdf_val = mat_pdf;
       PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
-      if (have_lights) pdf_val = fma(0.5, light_pdf<COUNT>(P, p, dir, cos_sl, C), 0.5 * mat_pdf);  // pdf.rs:116
+      if (have_lights)  // pdf.rs:116
+        pdf_val = fma(0.5, Trav::template lights_pdf<COUNT>(P, p, dir, cos_sl, C), 0.5 * mat_pdf);
 #ifdef RT_ABL_LPDF2  // ablation build: the light PDF evaluated twice (same result)
       if (have_lights) {
         d3 p2 = p;

@@ -46,8 +46,9 @@ def test_cornell_walker_sequence():
     blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
     state, src = rt.jit_check(blob)
     assert state == 1
+    world = src[:src.index("lights_pdf")]
     calls = re.findall(r"(aquad_test<COUNT, \d>|quad_test<COUNT>|sphere_test_v<COUNT>|translate_in|"
-                       r"rotate_y_in|o = ro;)", src)
+                       r"rotate_y_in|o = ro;)", world)
     assert calls[:6] == ["aquad_test<COUNT, 0>"] * 2 + ["aquad_test<COUNT, 1>"] * 3 + ["aquad_test<COUNT, 2>"]
     assert calls[6:8] == ["translate_in", "rotate_y_in"]
     assert len(calls) == 6 + 2 + 6 + 1 + 1 and calls[14] == "o = ro;" and calls[15] == "sphere_test_v<COUNT>"
@@ -56,4 +57,24 @@ def test_cornell_walker_sequence():
     lits = [float.fromhex(x) for x in re.findall(r"\((-?0x[0-9a-f.]+p[+-]\d+)\)", src)]
     assert all(struct.pack("<d", v) == struct.pack("<d", float.fromhex(v.hex())) for v in lits)
     # rcp of each axis formed once per frame: 3 in the world frame, 3 in the box frame
-    assert len(re.findall(r"r[xyz] = rcp_nr1", src)) == 6
+    assert len(re.findall(r"r[xyz] = rcp_nr1", world)) == 6
+
+
+def test_cornell_lights_pdf_unrolled():
+    """The mixture's light-list PDF (cornell_box lights = [light quad, glass sphere],
+    main.rs:485-494): the quad's axis-aligned test at t_min 0.001 and its area, the sphere's
+    root-free predicate with cos_theta_max shared from the shading block (first sphere light),
+    and the 1/len weight of HittableList::pdf_value (hittable.rs:116) as a literal."""
+    blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1
+    lp = src[src.index("lights_pdf"):]
+    assert lp.count("// light ") == 2
+    assert "aquad_test<COUNT, 1>" in lp and "0.001, kInf" in lp
+    assert "(0x1.aa9p+13)" in lp  # light area 130 x 105 = 13650
+    assert "cos_max = cos_sl0;" in lp
+    assert "return sum * (0x1p-1);" in lp
+    # a scene without lights: the value is never used (have_lights false), the function is 0
+    blob, cam = rt.preset_blob("random_balls", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1 and "// light " not in src[src.index("lights_pdf"):]
