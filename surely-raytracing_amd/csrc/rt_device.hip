@@ -545,7 +545,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       kslot = 40 + (tex ? 1 : 0) + (staged ? 2 : 0);
     }
   }
-  const int block = bvh ? kBlockBvh : kBlock;
+  int block = bvh ? kBlockBvh : kBlock;
+  if (jfn && bvh)
+    if (const char* b = std::getenv("RT_JIT_BVH_BLOCK")) block = std::atoi(b);  // diagnostics
   // (module kernels take their dynamic LDS size at launch; `kern` also serves as the fallback
   // should a scene-specialised launch be refused)
   if (lds_bytes > (64u << 10))

@@ -411,6 +411,12 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_SEED2
   opts.push_back("-DRT_ABL_SEED2");
 #endif
+  // diagnostics of the opt-in BVH kernels (rt_device.hip RT_JIT_BVH): another workgroup size
+  std::string blk;
+  if (const char* b = std::getenv("RT_JIT_BVH_BLOCK")) {
+    blk = std::string("-DRT_BLOCK_BVH=") + b;
+    opts.push_back(blk.c_str());
+  }
   const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t n = 0;
   hiprtcGetProgramLogSize(prog, &n);
