@@ -125,6 +125,95 @@ struct Gen {
   }
 };
 
+// The one-walk boundary query of the ConstantMedium record at `node` (rt_kernel.h
+// volume_two_hits: constant_medium.rs:46-55's rec1/rec2 as the two smallest candidates), its
+// instance chain and primitives unrolled with their constants as literals. Appends `struct
+// VolTwo_<node>` to `o`; false when the boundary is not a one-walk form.
+bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostringstream& o) {
+  const uint32_t kind = N[node] & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
+  if (!kind) return false;
+  std::ostringstream b;
+  size_t x = N[node + 3];
+  for (int guard = 0;; ++guard) {  // the instance chain in front of the primitive(s)
+    if (x + 4 > N.size() || guard > RTL_MAX_CHAIN + 8) return false;
+    const uint32_t ty = N[x] & 0xffu;
+    if (ty == RTL_TRANSLATE) {
+      b << "    translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4)) << ", o);\n";
+    } else if (ty == RTL_ROTATE_Y) {
+      b << "    rotate_y_in(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3)) << ", o, d);\n";
+    } else {
+      break;
+    }
+    x = N[x + 3];
+  }
+  const uint32_t ty = N[x] & 0xffu;
+  if (kind == RTL_VOLF_SPHERE) {
+    if (ty != RTL_SPHERE) return false;
+    b << "    d3 center = " << lit3(pd(N, x, 0), pd(N, x, 1), pd(N, x, 2)) << ";\n";
+    if (N[x] & RTL_SPHERE_MOVING)
+      b << "    center = vfma(tm, " << lit3(pd(N, x, 4), pd(N, x, 5), pd(N, x, 6)) << ", center);\n";
+    b << "    const double r = " << lit(pd(N, x, 3)) << ";\n"
+         "    const d3 oc = o - center;\n"
+         "    const double a = dot(d, d);\n"
+         "    const double half_b = dot(oc, d);\n"
+         "    const double c = dot(oc, oc) - r * r;\n"
+         "    const double disc = fma(half_b, half_b, -(a * c));\n"
+         "    const bool real = !(disc < 0.0);\n"
+         "    const double sqrtd = sqrt_nr(disc);\n"
+         "    const double ra = rcp_nr(a);\n"
+         "    const double near = (-half_b - sqrtd) * ra;\n"
+         "    const double far = (sqrtd - half_b) * ra;\n"
+         "    const bool n1 = (-kInf < near) & (near < kInf), f1 = (-kInf < far) & (far < kInf);\n"
+         "    t1 = n1 ? near : far;\n"
+         "    const double tmin2 = t1 + 0.0001;\n"
+         "    const bool n2 = (tmin2 < near) & (near < kInf), f2 = (tmin2 < far) & (far < kInf);\n"
+         "    t2 = n2 ? near : far;\n"
+         "    return real & (n1 | f1) & (n2 | f2);\n";
+  } else {
+    if (ty != RTL_QUAD && ty != RTL_QUADS) return false;
+    const bool batch = ty == RTL_QUADS;
+    const uint32_t cnt = batch ? (N[x] >> 8) : 1u;
+    const size_t q0 = batch ? x + 4 : x;
+    b << "    const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));\n"
+         "    double m1 = 0.0, m2 = 0.0;\n"
+         "    bool have1 = false, have2 = false;\n";
+    static const char* ax = "xyz";
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const size_t q = q0 + (size_t)k * RTL_QUAD_WORDS;
+      if (q + RTL_QUAD_WORDS > N.size()) return false;
+      const uint32_t axis = RTL_QUAD_AXIS(N[q]);
+      const int K = axis == 1u ? 0 : (axis == 2u ? 1 : 2);  // volume_two_hits' switch
+      b << "    {\n      const AQuad q = {" << N[q] << "u, " << lit(pd(N, q, 0)) << ", "
+        << lit(pd(N, q, 1)) << ", " << lit(pd(N, q, 2)) << ", " << lit(pd(N, q, 3)) << ", "
+        << lit(pd(N, q, 4)) << "};\n"
+        << "      double t, a, b;\n      aquad_core<" << K << ">(q, o, d, r, t, a, b);\n"
+        << "      const double dk = d." << ax[K] << ";\n"
+           "      const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);\n"
+           "      const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);\n"
+           "      const bool lt1 = v & (!have1 | (t < m1));\n"
+           "      const bool lt2 = v & !lt1 & (!have2 | (t < m2));\n"
+           "      m2 = lt1 ? m1 : (lt2 ? t : m2);\n"
+           "      have2 = have2 | (lt1 & have1) | lt2;\n"
+           "      m1 = lt1 ? t : m1;\n"
+           "      have1 = have1 | v;\n    }\n";
+    }
+    b << "    t1 = m1;\n"
+         "    const double tmin2 = m1 + 0.0001;\n"
+         "    bool hit2;\n"
+         "    if (m1 >= tmin2) {\n      t2 = m1;\n      hit2 = true;\n"
+         "    } else if (have2 && m2 >= tmin2) {\n      t2 = m2;\n      hit2 = true;\n"
+         "    } else {\n      t2 = 0.0;\n      hit2 = false;\n      fallback = have2;\n    }\n"
+         "    return have1 & (hit2 | fallback);\n";
+  }
+  o << "struct VolTwo_" << node << " {\n"
+       "  static __device__ __forceinline__ bool two_hits(const TraceParams& P, uint32_t node,\n"
+       "      uint32_t kind, d3 o, d3 d, double tm, double& t1, double& t2, bool& fallback) {\n"
+       "    (void)P; (void)node; (void)kind; (void)tm;\n"
+       "    fallback = false;\n"
+    << b.str() << "  }\n};\n";
+  return true;
+}
+
 // The light-list PDF value of the mixture (rt_kernel.h light_pdf: HittableList::pdf_value
 // hittable.rs:115-124 over Quad/Sphere::pdf_value object.rs:492-501, 190-202), the list unrolled
 // with each light's constants as literals: the same expressions in the same order.
@@ -222,6 +311,7 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
   }
   Gen G(N);
   std::ostringstream& o = G.o;
+  std::ostringstream pre;  // policies the walker refers to (generated volume boundary queries)
   o << "struct TravGen {\n"
        "  template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>\n"
        "  static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,\n"
@@ -271,7 +361,10 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
       node = N[node + 3];
     } else if (ty == RTL_VOLUME) {
       // ConstantMedium (constant_medium.rs:41-95): the interpreter's boundary walks
-      o << "    h = volume_hit<COUNT, true, BVH, VOLI>(P, " << node << "u, make_uint4(" << N[node] << "u, "
+      const bool vt = gen_volume_two_hits(N, node, pre);
+      o << "    h = volume_hit<COUNT, true, BVH, VOLI"
+        << (vt ? ", VolTwo_" + std::to_string(node) : std::string()) << ">(P, " << node
+        << "u, make_uint4(" << N[node] << "u, "
         << N[node + 1] << "u, " << N[node + 2] << "u, " << N[node + 3] << "u), ro, rd, tm, o, d, "
         << frame << ", tmin, closest, t, g, C);\n"
         << "    closest = h ? t : closest;\n    code = h ? " << G.code(node, frame) << "u : code;\n";
@@ -323,7 +416,7 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
        "  }\n";
   if (!gen_lights_pdf(F, o, why)) return "";
   o << "};\n";
-  return o.str();
+  return pre.str() + o.str();
 }
 
 Flags product_flags(const rtf::FlatScene& F, bool staged) {

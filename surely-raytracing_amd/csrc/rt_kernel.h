@@ -652,6 +652,15 @@ __device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t ki
   }
   return have1 & (hit2 | fallback);
 }
+// The one-walk boundary query of the interpreter; scene-specialised kernels (rt_jit.cpp) pass
+// a generated policy per ConstantMedium record with the same arithmetic.
+struct VolTwoInterp {
+  static __device__ __forceinline__ bool two_hits(const TraceParams& P, uint32_t node,
+                                                  uint32_t kind, d3 o, d3 d, double tm,
+                                                  double& t1, double& t2, bool& fallback) {
+    return volume_two_hits(P, node, kind, o, d, tm, t1, t2, fallback);
+  }
+};
 
 #ifdef RT_PROF
 // profiling build: per-lane LANE-walker step counts and per-workgroup traversal counters
@@ -705,7 +714,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
 // current frame (o, d): true when the free-flight distance ends inside the boundary before
 // `closest`, with the hit t in t_hit. Shared by the interpreter walker and the generated
 // walkers of rt_jit.cpp.
-template <bool COUNT, bool UNI, bool BVH, bool VOLI>
+template <bool COUNT, bool UNI, bool BVH, bool VOLI, class VT = VolTwoInterp>
 __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, uint4 h, d3 wo,
                                            d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                                            double closest, double& t_hit, Rng& g, Ctr<COUNT>& C) {
@@ -719,10 +728,10 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
   const uint32_t fuse = h.x & (RTL_VOLF_SPHERE | RTL_VOLF_QUADS);
   if constexpr (UNI && !COUNT && !VOLI) {  // every boundary is a one-walk sphere
     bool fb;
-    both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+    both = VT::two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
   } else if (UNI && !COUNT && fuse) {
     bool fb;
-    both = volume_two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
+    both = VT::two_hits(P, h.w, fuse, o, d, tm, t1, t2, fb);
     if (__ballot(fb) != 0ull) {  // rare: rerun the second query for those lanes
       double tb;
       uint32_t dn;

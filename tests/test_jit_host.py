@@ -78,3 +78,25 @@ def test_cornell_lights_pdf_unrolled():
     blob, cam = rt.preset_blob("random_balls", width=32, spp=4)
     state, src = rt.jit_check(blob)
     assert state == 1 and "// light " not in src[src.index("lights_pdf"):]
+
+
+def test_volume_boundary_queries_generated():
+    """ConstantMedium records (constant_medium.rs:41-95) with a one-walk boundary get a generated
+    two-smallest-candidates query: cornell_smoke's two boxes (main.rs:514-598) as Translate +
+    RotateY + six axis quads each, final_scene's two sphere boundaries (main.rs:656-670)."""
+    blob, cam = rt.preset_blob("cornell_smoke", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1, src
+    structs = re.findall(r"struct (VolTwo_\d+) \{", src)
+    assert len(structs) == 2
+    for name in structs:
+        assert f"volume_hit<COUNT, true, BVH, VOLI, {name}>" in src
+        body = src[src.index(f"struct {name}"):]
+        body = body[:body.index("\n};")]
+        assert body.count("aquad_core<") == 6
+        assert body.index("translate_in") < body.index("rotate_y_in")
+    blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1, src
+    structs = re.findall(r"struct (VolTwo_\d+) \{", src)
+    assert len(structs) == 2 and all("sqrt_nr(disc)" in src for _ in structs)
