@@ -1539,7 +1539,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const TP S0 = T.lights + T.loffs[P.sphere_light0];
       const d3 cmo = ld3(S0, 0) - p;
       const double r0 = ldd(S0, 3);
-      const double arg = 1.0 - r0 * r0 / dot(cmo, cmo);
+      const double arg = 1.0 - div_nr(r0 * r0, dot(cmo, cmo));
       sq_in = diel ? sq_in : arg;
     }
     const double sq = sqrt_nr(sq_in);
