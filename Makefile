@@ -72,3 +72,12 @@ variants-occ: $(DEV_SRC) $(DEV_HDR)
 prof: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/prof
 	$(HIPCC) $(HIPFLAGS) -DRT_PROF -shared $(DEV_SRC) -o $(BUILD)/prof/librtmi355x.so -lhiprtc
+
+# occupancy variants of the non-BVH kernels (the scene-specialised C2/C3 kernels inherit
+# RT_MIN_WAVES through rt_jit.cpp); A/B with
+# VARDIR=build/variants_jocc python tools_gpu/ab_variants.py W SPP ROUNDS SCENE
+variants-jocc: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_jocc
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=3 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w3.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=5 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w5.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=6 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w6.so -lhiprtc
