@@ -510,6 +510,13 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
     blk = std::string("-DRT_BLOCK_BVH=") + b;
     opts.push_back(blk.c_str());
   }
+  // diagnostics: extra compiler options, space separated (register-allocation A/B)
+  std::vector<std::string> extra;
+  if (const char* e = std::getenv("RT_JIT_OPTS")) {
+    std::istringstream in(e);
+    for (std::string w; in >> w;) extra.push_back(w);
+  }
+  for (const std::string& w : extra) opts.push_back(w.c_str());
   const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t n = 0;
   hiprtcGetProgramLogSize(prog, &n);
