@@ -256,7 +256,12 @@ static inline vec3 vscale(vec3 a, real t) { return v3(a.x * t, a.y * t, a.z * t)
 static inline vec3 vfma(real t, vec3 a, vec3 b) { /* t*a + b */
   return v3(FMA(t, a.x, b.x), FMA(t, a.y, b.y), FMA(t, a.z, b.z));
 }
+#if ORACLE_F64
+/* vec3.rs:167-169 / 74-76: (x*x' + y*y') + z*z', evaluated left to right */
+static inline real dot(vec3 a, vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+#else
 static inline real dot(vec3 a, vec3 b) { return FMA(a.x, b.x, FMA(a.y, b.y, a.z * b.z)); }
+#endif
 static inline vec3 cross(vec3 u, vec3 v) {
   return v3(FMA(u.y, v.z, -(u.z * v.y)), FMA(u.z, v.x, -(u.x * v.z)), FMA(u.x, v.y, -(u.y * v.x)));
 }
@@ -1050,9 +1055,9 @@ typedef struct {
 static void render_pixel(ctx_t* cx, job_t* jb, int x, int y, float* out) {
   const ocam* c = &jb->cam;
   uint32_t pixel = (uint32_t)(y * c->W + x);
+  /* render.rs:185-189: one running sum per pixel over s_j (outer) and s_i (inner) */
   real tot[3] = {R(0), R(0), R(0)};
   for (int s_j = jb->sj0; s_j < jb->sj1; ++s_j) {
-    real row[3] = {R(0), R(0), R(0)};
     for (int s_i = 0; s_i < c->sqrt_spp; ++s_i) {
       rng_t g;
       rng_seed(&g, jb->opts->seed, pixel, (uint32_t)(s_j * c->sqrt_spp + s_i));
@@ -1060,13 +1065,10 @@ static void render_pixel(ctx_t* cx, job_t* jb, int x, int y, float* out) {
       CNT(cx, RT_OP_SAMPLES);
       ray_t r = get_ray(c, x, y, s_i, s_j, &g);
       vec3 col = ray_color(cx, &jb->cc, &r, jb->cc.max_depth, &g);
-      row[0] += col.x;
-      row[1] += col.y;
-      row[2] += col.z;
+      tot[0] += col.x;
+      tot[1] += col.y;
+      tot[2] += col.z;
     }
-    tot[0] += row[0];
-    tot[1] += row[1];
-    tot[2] += row[2];
   }
   int ow = jb->opts->flags & RT_FLAG_OVERWRITE;
   for (int k = 0; k < 3; ++k) out[k] = ow ? (float)tot[k] : (float)((real)out[k] + tot[k]);

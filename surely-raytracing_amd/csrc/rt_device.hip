@@ -46,27 +46,27 @@ __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::valu
   trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterp>(P);
 }
 
-// Per pixel: sum the samples of each stratum row (s_i inner) and the rows (s_j outer), the
-// order of render.rs:185-189, in f64. One wave per 8x8 tile, lane = pixel of the tile: the
-// samples of one (tile, s_j, s_i) sit in pool-item order (item = s_i * nv + pv), so every load
-// instruction reads nv * 12 contiguous bytes. Chunked calls carry the running sum in `tot`.
-// mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite.
-__global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
+// Per pixel: the f64 sum of each stratum row s_j (a row item's partial, or the sequential s_i
+// sum of a tail pair's per-sample values: the same running sum, bit for bit), then the rows in
+// s_j order (render.rs:185-189 adds every sample into one running sum; here the rows are summed
+// first, so the association differs from the reference only between rows). One wave per 8x8
+// tile, lane = pixel of the tile: each load instruction reads 64 * 8 contiguous bytes. Chunked
+// calls carry the running sum in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum),
+// bit2 overwrite.
+__global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part,
                                                  double* __restrict__ tot,
                                                  float* __restrict__ accum, int W, int n_rows,
                                                  int tiles_x, int n_tiles, int n_sj, int S,
-                                                 int mode) {
+                                                 int n_pairs_a, int mode) {
   const int tile_id = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int pv = threadIdx.x & 63;
   if (tile_id >= n_tiles) return;
   const int tx = tile_id % tiles_x, ty = tile_id / tiles_x;
   const int tile_w = min(kWaveTile, W - tx * kWaveTile);
   const int tile_h = min(kWaveTile, n_rows - ty * kWaveTile);
-  const int nv = tile_w * tile_h;
-  if (pv >= nv) return;
+  if (pv >= tile_w * tile_h) return;
   const int x = tx * kWaveTile + pv % tile_w, kr = ty * kWaveTile + pv / tile_w;
   const size_t i = (size_t)kr * W + x;
-  const size_t tile = (size_t)tile_id;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   if (!(mode & 1)) {
     t0 = tot[3 * i];
@@ -74,14 +74,19 @@ __global__ __launch_bounds__(256) void rt_reduce(const float* __restrict__ samp,
     t2 = tot[3 * i + 2];
   }
   for (int k = 0; k < n_sj; ++k) {
-    const float* r = samp + ((tile * n_sj + k) * (size_t)(kWaveTile * kWaveTile) * S + pv) * 3;
-    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
-#pragma unroll 8
-    for (int si = 0; si < S; ++si) {
-      const float* q = r + (size_t)si * nv * 3;
-      r0 += (double)q[0];
-      r1 += (double)q[1];
-      r2 += (double)q[2];
+    const size_t q = (size_t)tile_id * n_sj + k;
+    double r0, r1, r2;
+    if (q < (size_t)n_pairs_a) {
+      const double* r = part + (q * 64 + pv) * 3;
+      r0 = r[0], r1 = r[1], r2 = r[2];
+    } else {
+      const double* r = part + ((size_t)n_pairs_a * 64 + (q - n_pairs_a) * (size_t)S * 64 + pv) * 3;
+      r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll 4
+      for (int si = 0; si < S; ++si) {
+        const double* v = r + (size_t)si * 64 * 3;
+        r0 += v[0], r1 += v[1], r2 += v[2];
+      }
     }
     t0 += r0;
     t1 += r1;
@@ -132,6 +137,7 @@ struct rt_scene {
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
+  size_t lds_module_max = 64u << 10;  // LDS a module (hiprtc) launch may take (device limit)
   int resident_blocks[48] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
   size_t resident_lds[48] = {};  // ... at this dynamic LDS size
   // scene-specialised product kernel (rt_jit.cpp): the generated world walker, compiled on the
@@ -238,6 +244,11 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   if (e == hipSuccess) e = hipMalloc(&sc->ops, sizeof(unsigned long long) * 32 + 256);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&sc->n_cu, hipDeviceAttributeMultiprocessorCount,
                                                  device);
+  int lds_block = 0;
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+  if (e == hipSuccess && lds_block > 0)
+    sc->lds_module_max = std::min<size_t>((size_t)lds_block, kLdsTotal);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
   for (int k = 0; k < rt_scene::kTraceRing && e == hipSuccess; ++k) {
@@ -268,8 +279,6 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   } else {
     sc->jit_walker = rtj::generate(F, &sc->jit_msg);
     sc->jit_state = sc->jit_walker.empty() ? -1 : 0;
-    if (sc->jit_state == 0 && F.hdr.has_bvh)
-      sc->jit_msg = "BVH scene: interpreter kernel (RT_JIT_BVH=1 opts in to the generated walker)";
   }
   sc->sphere_light0 = -1;
   for (size_t i = 0; i < F.light_offs.size(); ++i)
@@ -348,6 +357,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     return set_err(RT_ERR_INVALID_ARG, "row range outside the image");
   if ((int64_t)W * cam->image_height >= (1ll << 32) || (int64_t)S * S >= (1ll << 32))
     return set_err(RT_ERR_UNSUPPORTED, "image or spp too large for 32-bit pixel/sample keys");
+  // lane item keys pack x (16 bits), the call's row index (15 bits) and s_j / s_i (16 bits each)
+  if (W > 65535 || opts->n_rows > 32767)
+    return set_err(RT_ERR_UNSUPPORTED, "image_width > 65535 or n_rows > 32767 in one call");
   const int sj0 = opts->sj_count > 0 ? opts->sj_begin : 0;
   const int n_sj = opts->sj_count > 0 ? opts->sj_count : S;
   if (sj0 < 0 || sj0 + n_sj > S) return set_err(RT_ERR_INVALID_ARG, "bad stratum range");
@@ -361,26 +373,6 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   if (stats) std::memset(stats, 0, sizeof(*stats));
   const size_t n_px = (size_t)opts->n_rows * W;
   if (n_px == 0) return RT_OK;
-  // Workspace: one float3 slot per sample of a chunk of stratum rows, plus an f64 running sum
-  // per pixel. Chunks keep it under RT_WORKSPACE_MB (default 8 GiB) even for the 3840x2160 x
-  // 10000 spp config; the C2 frame (800x800x961) fits one chunk (7.4 GB).
-  size_t cap = (size_t)8192 << 20;
-  if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
-  const size_t n_tiles = (size_t)((W + kWaveTile - 1) / kWaveTile) *
-                         (size_t)((opts->n_rows + kWaveTile - 1) / kWaveTile);
-  const size_t per_sj = n_tiles * (size_t)(kWaveTile * kWaveTile) * (size_t)S * 3 * sizeof(float);
-  const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
-  int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_sj, (cap > tot_bytes ? cap - tot_bytes : 0) / per_sj));
-  const size_t need = tot_bytes + per_sj * (size_t)chunk;
-  if (need > sc->work_bytes) {
-    if (sc->work) HIP_TRY(hipFree(sc->work));
-    sc->work = nullptr;
-    sc->work_bytes = 0;
-    HIP_TRY(hipMalloc(&sc->work, need));
-    sc->work_bytes = need;
-  }
-  double* tot = (double*)sc->work;
-  float* samp = (float*)(sc->work + tot_bytes);
   TraceParams P;
   std::memset(&P, 0, sizeof(P));
   P.nodes = sc->nodes;
@@ -390,7 +382,6 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.lights = sc->lights;
   P.light_offs = sc->light_offs;
   P.texels = sc->texels;
-  P.samp = samp;
   P.ops = sc->ops;
   P.queue = sc->queue;
   P.root = sc->hdr.root;
@@ -399,6 +390,19 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.inv_n_lights = sc->hdr.n_lights ? 1.0 / (double)sc->hdr.n_lights : 0.0;
   P.sphere_light0 = sc->sphere_light0;
   P.flags = opts->flags;
+#ifdef RT_PROF
+  const bool count = true;
+#else
+  const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
+#endif
+  // VOL kernels: ConstantMedium nodes or an Isotropic material (also usable outside one)
+  const bool vol = (sc->hdr.has_volume | sc->hdr.has_isotropic) != 0;
+  const bool tex = sc->hdr.has_textures != 0;
+  const bool bvh = sc->hdr.has_bvh != 0;
+  const int block = bvh ? kBlockBvh : kBlock;
+  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc), the op
+  // counters, slack for the profiling build; the dynamic LDS holds the staged tables
+  const size_t static_lds = (size_t)block * 24 + 512 + (count ? 128 : 0);
   // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
   // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.
   const uint32_t used_perlins = sc->hdr.has_textures ? sc->hdr.n_perlins : 0u;
@@ -413,19 +417,17 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     P.stage_src = sc->perlin;
     P.stage_bytes = P.n_perlin_lds * RTL_PERLIN_BYTES;
   }
+  // product renders of a generated scene run its scene-specialised kernel (same template
+  // arguments and launch bounds as the ahead-of-time kernel, top-level walk unrolled; rt_jit.cpp)
+  const bool want_jit = !count && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0;
   // BVH region (rt_layout.h): in LDS with the small scene, else staged after the Perlin tables
-  // as far as the LDS budget of the 512-thread BVH workgroup allows (the rest is read from HBM)
+  // as far as the workgroup's LDS budget allows (the rest is read through the caches)
   P.bvh_words = sc->hdr.bvh_words;
   if (P.stage_scene) {
     P.bvh_lds_words = P.bvh_words;
     P.bvh_lds_off = 0;
-  } else if (sc->hdr.has_bvh) {
-    // a scene-specialised kernel (module launch) is given at most 64 KiB of dynamic LDS (the
-    // ahead-of-time kernels take hipFuncSetAttribute's opt-in for more)
-    const char* jb = std::getenv("RT_JIT_BVH");
-    const bool jit_lds = !(opts->flags & (RT_FLAG_COUNT_OPS | RT_FLAG_INTERPRETER)) &&
-                         sc->jit_state >= 0 && jb && std::strcmp(jb, "1") == 0;
-    const size_t cap = jit_lds ? std::min<size_t>(kLdsBvhMax, 64u << 10) : kLdsBvhMax;
+  } else if (bvh) {
+    const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
     const size_t room = cap > P.stage_bytes ? cap - P.stage_bytes : 0;
     P.bvh_lds_words = (uint32_t)std::min<size_t>(P.bvh_words, room / 64 * 16);
     P.bvh_lds_off = P.stage_bytes;
@@ -453,27 +455,13 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.row_begin = opts->row_begin;
   P.row_step = opts->row_step;
   P.sqrt_spp = S;
-  P.sj0 = sj0;
-  P.n_sj = n_sj;
   P.max_depth = cam->max_depth;
   P.seed_lo = (uint32_t)opts->seed;
   P.seed_hi = (uint32_t)(opts->seed >> 32);
   P.tiles_x = (W + kWaveTile - 1) / kWaveTile;
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
+  const int n_tiles = P.tiles_x * tiles_y;
   P.n_blk = (S + kPoolSi - 1) / kPoolSi;
-  const int64_t waves_per_sj = (int64_t)P.tiles_x * tiles_y * P.n_blk;  // pools per s_j row
-  if (waves_per_sj * chunk > 0x7fffffff) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
-#ifdef RT_PROF
-  const bool count = true;
-#else
-  const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
-#endif
-  if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
-  if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
-  // VOL kernels: ConstantMedium nodes or an Isotropic material (also usable outside one)
-  const bool vol = (sc->hdr.has_volume | sc->hdr.has_isotropic) != 0;
-  const bool tex = sc->hdr.has_textures != 0;
-  const bool bvh = sc->hdr.has_bvh != 0;
   typedef void (*kern_t)(TraceParams);
   // [count][vol][tex][bvh]; a scene without a BVH whose tables are staged in LDS runs the
   // STAGED variant (LDS-typed table reads), BVH kernels read the tables from global memory
@@ -511,19 +499,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int vb = (novoli ? 4 : 0) + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0);
   kern_t kern = staged ? table_staged[kidx / 2 - 8] : (novolb ? table_bvh_novolb[vb] : table[kidx]);
   int kslot = novolb ? 32 + vb : kidx;
-  // product renders of a generated scene run its scene-specialised kernel (same template
-  // arguments and launch bounds as `kern`, top-level walk unrolled; rt_jit.cpp)
   hipFunction_t jfn = nullptr;
-  // BVH scenes: the generated walker (BVH subtrees call the per-lane walker) compiles, but on
-  // this ROCm the queue aborts its 768-thread module launch (HSA_STATUS_ERROR_INVALID_ISA, while
-  // the same template's ahead-of-time kernel runs), so it is opt-in (RT_JIT_BVH=1) until that is
-  // understood
-  static const bool jit_bvh = [] {
-    const char* e = std::getenv("RT_JIT_BVH");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  if (!count && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0 &&
-      lds_bytes <= (64u << 10) && (!bvh || jit_bvh)) {
+  if (want_jit && lds_bytes + static_lds <= sc->lds_module_max) {
     rtj::Kernel& jk = sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)];
     if (!jk.fn) {
       std::string log;
@@ -537,6 +514,26 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       if (rtj::get_kernel(sc->jit_walker, sc->device, jf, &jk, &log) != 0) {
         sc->jit_state = -2;
         sc->jit_msg = log;
+      } else {
+        // a dispatch the hardware cannot place aborts the whole queue (the CP's register or
+        // LDS check), so the code object's resources are checked against this launch first:
+        // workgroup size, VGPRs x waves per SIMD within the 512-entry file, LDS within the CU
+        const int waves_per_simd = (block / 64 + 3) / 4;
+        const int regs = (jk.regs + 7) & ~7;
+        char why[256];
+        std::snprintf(why, sizeof(why),
+                      "scene-specialised kernel: %d regs, max %d threads, %d B static LDS, "
+                      "%d B scratch/lane; launch %d threads, %zu B dynamic LDS",
+                      jk.regs, jk.max_threads, jk.static_lds, jk.scratch, block, lds_bytes);
+        if (jk.max_threads < block || regs * waves_per_simd > 512 ||
+            (size_t)jk.static_lds + lds_bytes > sc->lds_module_max ||
+            (size_t)jk.static_lds > static_lds) {
+          sc->jit_state = -2;
+          sc->jit_msg = std::string("not launched: ") + why;
+          jk = rtj::Kernel{};
+        } else {
+          sc->jit_msg = why;
+        }
       }
     }
     if (jk.fn) {
@@ -545,12 +542,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       kslot = 40 + (tex ? 1 : 0) + (staged ? 2 : 0);
     }
   }
-  int block = bvh ? kBlockBvh : kBlock;
-  if (jfn && bvh)
-    if (const char* b = std::getenv("RT_JIT_BVH_BLOCK")) block = std::atoi(b);  // diagnostics
-  // (module kernels take their dynamic LDS size at launch; `kern` also serves as the fallback
-  // should a scene-specialised launch be refused)
-  if (lds_bytes > (64u << 10))
+  // (module kernels take their dynamic LDS size at launch)
+  if (!jfn && lds_bytes > (64u << 10))
     HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_bytes));
   if (sc->resident_blocks[kslot] == 0 || sc->resident_lds[kslot] != lds_bytes) {
@@ -558,34 +551,67 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     const hipError_t oe =
         jfn ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jfn, block, lds_bytes)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, block, lds_bytes);
-    if (oe != hipSuccess || nb <= 0) nb = 1;
+    if (oe != hipSuccess || nb <= 0)
+      return set_err(RT_ERR_HIP, std::string("occupancy query: the path kernel does not fit a CU (") +
+                                     (oe != hipSuccess ? hipGetErrorString(oe) : "0 blocks") + ")");
     sc->resident_blocks[kslot] = nb;
     sc->resident_lds[kslot] = lds_bytes;
   }
   const int64_t max_blocks = (int64_t)sc->resident_blocks[kslot] * std::max(1, sc->n_cu);
+  // Outputs (TraceParams::part): one f64 RGB partial per (pixel, s_j) of the row pairs and one
+  // per sample of the tail pairs. The tail is about one pair per resident wave (a pair is 64 x
+  // sqrt_spp paths): when the row pools run out, lanes still finishing a row have ~sqrt_spp / 2
+  // samples left, and the tail's single samples keep the other lanes busy meanwhile.
+  // RT_TAIL_PAIRS overrides it (tests: the image does not depend on the split).
+  int64_t tail = max_blocks * (block / 64);
+  if (const char* e = std::getenv("RT_TAIL_PAIRS")) tail = std::strtoll(e, nullptr, 10);
+  tail = std::max<int64_t>(0, tail);
+  // Chunks of stratum rows keep the workspace under RT_WORKSPACE_MB (default 8 GiB): the
+  // 3840x2160 x 10000 spp frame takes several; 800x800 x 961 spp takes one (~0.7 GB).
+  size_t cap = (size_t)8192 << 20;
+  if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
+  const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
+  const size_t row_bytes = (size_t)64 * 3 * sizeof(double);  // one pair's row partials
+  const size_t tail_bytes = (size_t)S * row_bytes;           // one tail pair's samples
+  auto part_bytes = [&](int cn) {
+    const int64_t pairs = (int64_t)n_tiles * cn;
+    const int64_t tb = std::min<int64_t>(pairs, tail);
+    return (size_t)(pairs - tb) * row_bytes + (size_t)tb * tail_bytes;
+  };
+  int chunk = n_sj;
+  while (chunk > 1 && tot_bytes + part_bytes(chunk) > cap) chunk = (chunk + 1) / 2;
+  const size_t need = tot_bytes + part_bytes(chunk);
+  if ((int64_t)n_tiles * chunk * 64 * (int64_t)std::max(1, S) >= (1ll << 32) ||
+      (int64_t)n_tiles * chunk * P.n_blk > 0x7fffffff)
+    return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+  if (need > sc->work_bytes) {
+    if (sc->work) HIP_TRY(hipFree(sc->work));
+    sc->work = nullptr;
+    sc->work_bytes = 0;
+    HIP_TRY(hipMalloc(&sc->work, need));
+    sc->work_bytes = need;
+  }
+  double* tot = (double*)sc->work;
+  P.part = (double*)(sc->work + tot_bytes);
+  if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
+  if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
     const int cn = std::min(chunk, sj0 + n_sj - c0);
+    const int64_t pairs = (int64_t)n_tiles * cn;
+    const int64_t tb = std::min<int64_t>(pairs, tail);
     P.sj0 = c0;
     P.n_sj = cn;
-    P.n_pools = (int)(waves_per_sj * cn);
+    P.n_pairs_a = (int)(pairs - tb);
+    P.n_pools = (int)(P.n_pairs_a + tb * P.n_blk);
     // persistent grid: as many waves as the device holds at once (never more than pools)
-    const int64_t blocks =
-        std::min(max_blocks, (waves_per_sj * cn + (block / 64) - 1) / (block / 64));
+    const int64_t blocks = std::min(max_blocks, ((int64_t)P.n_pools + (block / 64) - 1) / (block / 64));
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
     const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
     if (jfn) {
       void* args[] = {&P};
-      const hipError_t le = hipModuleLaunchKernel(jfn, (unsigned)blocks, 1, 1, (unsigned)block, 1,
-                                                  1, (unsigned)lds_bytes, stream, args, nullptr);
-      if (le != hipSuccess) {  // refused at launch (nothing ran): the interpreter kernel renders
-        (void)hipGetLastError();
-        sc->jit_state = -2;
-        sc->jit_msg = std::string("hipModuleLaunchKernel: ") + hipGetErrorString(le);
-        sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)] = rtj::Kernel{};
-        jfn = nullptr;
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
-      }
+      HIP_TRY(hipModuleLaunchKernel(jfn, (unsigned)blocks, 1, 1, (unsigned)block, 1, 1,
+                                    (unsigned)lds_bytes, stream, args, nullptr));
     } else {
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds_bytes, stream, P);
     }
@@ -595,9 +621,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     ++sc->n_tev;
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
                      ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
-    const int n_tiles = P.tiles_x * tiles_y;
-    hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, stream, samp,
-                       tot, accum, W, opts->n_rows, P.tiles_x, n_tiles, cn, S, mode);
+    hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, stream, P.part,
+                       tot, accum, W, opts->n_rows, P.tiles_x, n_tiles, cn, S, P.n_pairs_a, mode);
     HIP_TRY(hipGetLastError());
   }
   ++sc->n_render;

@@ -474,8 +474,14 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   const std::string off = "--offload-arch=" + arch;
   // the ahead-of-time build's arithmetic flags (Makefile HIPFLAGS): contraction off, so every
   // fma is the one written in rt_kernel.h and the generated walker computes the same bits
+  // No VGPR spills into AGPRs: the hiprtc a process binds to is whichever libhiprtc is loaded
+  // first (PyTorch's bundled ROCm 7.0 comgr once torch is imported), and that compiler put 3
+  // AGPRs on top of the 168 VGPRs of the 768-thread BVH kernel: 171 registers x 3 waves per SIMD
+  // exceed the 512-entry file, so the CP rejected the dispatch (REGISTER_INVALID, reported as
+  // HSA_STATUS_ERROR_INVALID_ISA) and aborted the queue. Spills then go to scratch instead.
   std::vector<const char*> opts = {off.c_str(), "-O3", "-std=c++17", "-ffp-contract=off",
-                                   "-fno-gpu-flush-denormals-to-zero"};
+                                   "-fno-gpu-flush-denormals-to-zero", "-mllvm",
+                                   "-amdgpu-spill-vgpr-to-agpr=0"};
   // build knobs of this library (ablation / occupancy variants, Makefile) apply to its
   // run-time kernels too
 #define RTJ_STR2(x) #x
@@ -485,6 +491,12 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #endif
 #ifdef RT_MIN_WAVES
   opts.push_back("-DRT_MIN_WAVES=" RTJ_STR(RT_MIN_WAVES));
+#endif
+#ifdef RT_MIN_WAVES_BVH
+  opts.push_back("-DRT_MIN_WAVES_BVH=" RTJ_STR(RT_MIN_WAVES_BVH));
+#endif
+#ifdef RT_BLOCK_BVH
+  opts.push_back("-DRT_BLOCK_BVH=" RTJ_STR(RT_BLOCK_BVH));
 #endif
 #ifdef RT_PROF
   opts.push_back("-DRT_PROF");
@@ -504,12 +516,6 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_SEED2
   opts.push_back("-DRT_ABL_SEED2");
 #endif
-  // diagnostics of the opt-in BVH kernels (rt_device.hip RT_JIT_BVH): another workgroup size
-  std::string blk;
-  if (const char* b = std::getenv("RT_JIT_BVH_BLOCK")) {
-    blk = std::string("-DRT_BLOCK_BVH=") + b;
-    opts.push_back(blk.c_str());
-  }
   // diagnostics: extra compiler options, space separated (register-allocation A/B)
   std::vector<std::string> extra;
   if (const char* e = std::getenv("RT_JIT_OPTS")) {
@@ -568,6 +574,14 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
   if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&k.fn, k.mod, "rt_trace_jit") != hipSuccess) {
     *log = "hipModuleLoadData / hipModuleGetFunction failed";
+    return RT_ERR_HIP;
+  }
+  if (hipFuncGetAttribute(&k.regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, k.fn) != hipSuccess ||
+      hipFuncGetAttribute(&k.max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, k.fn) !=
+          hipSuccess ||
+      hipFuncGetAttribute(&k.static_lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, k.fn) != hipSuccess ||
+      hipFuncGetAttribute(&k.scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k.fn) != hipSuccess) {
+    *log = "hipFuncGetAttribute failed on the scene-specialised kernel";
     return RT_ERR_HIP;
   }
   cache.emplace(key, k);

@@ -30,6 +30,9 @@ Flags product_flags(const rtf::FlatScene& F, bool staged);
 struct Kernel {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
+  // code-object resources as the runtime reports them (hipFuncGetAttribute), checked against
+  // the launch before every first use (rt_device.hip)
+  int regs = 0, max_threads = 0, static_lds = 0, scratch = 0;
 };
 int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
                std::string* log);

@@ -55,8 +55,9 @@ template <bool BVH>
 struct BlockOf {
   static constexpr int value = BVH ? kBlockBvh : kBlock;
 };
-// Dynamic LDS budgets: whole small scenes (kStageScene) / the BVH region of a BVH kernel.
-constexpr size_t kLdsBvhMax = 152u << 10;
+// LDS of one workgroup (gfx950: 160 KiB per CU): static (per-lane running sums, counters) plus
+// dynamic (whole small scenes, kStageScene; or the Perlin tables and the BVH region).
+constexpr size_t kLdsTotal = 160u << 10;
 // Minimum waves per SIMD for the path kernel (__launch_bounds__ 2nd argument). 4 caps the
 // allocation at 128 VGPRs. Kernels with a per-lane BVH walker run 3 (168 VGPRs; see kBlockBvh);
 // kernels without a BVH stay at 4 (cornell_box at 3 or 5: -13 %; cornell_smoke at 3: -8 %,
@@ -221,11 +222,15 @@ struct TraceParams {
   const uint32_t* __restrict__ lights;
   const uint32_t* __restrict__ light_offs;
   const uint8_t* __restrict__ texels;
-  float* __restrict__ samp;  // per-sample radiance, [wave][pool item] x RGB (item = s_i*nv + pv)
+  // f64 RGB outputs of the launch (rt_reduce sums them): first the stratum-row partials of the
+  // row pairs [0, n_pairs_a) (index pair * 64 + pv), then the per-sample values of the tail
+  // pairs (index n_pairs_a * 64 + ((pair - n_pairs_a) * sqrt_spp + s_i) * 64 + pv)
+  double* __restrict__ part;
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  int n_pools;                       // pools of this launch: tiles x n_sj x n_blk
-  int n_blk;                         // s_i blocks per (tile, s_j): ceil(sqrt_spp / kPoolSi)
+  int n_pools;    // pools of this launch: n_pairs_a row pools, then (pairs - n_pairs_a) * n_blk
+  int n_pairs_a;  // (tile, s_j) pairs rendered as whole stratum rows per lane
+  int n_blk;      // s_i blocks per tail pair: ceil(sqrt_spp / kPoolSi)
   uint32_t root, n_lights, lights_is_list, flags;
   int sphere_light0;    // index of the first SPHERE light record, -1 if none
   double inv_n_lights;  // 1.0 / n_lights (host IEEE division, hittable.rs:116)
@@ -1206,11 +1211,31 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
   return P.lights_is_list ? sum * P.inv_n_lights : sum;  // weight = 1/len (hittable.rs:116)
 }
 
-__device__ __forceinline__ void store_sample(float* __restrict__ samp, size_t slot, d3 L) {
-  float* o = samp + slot * 3;
-  o[0] = (float)L.x;
-  o[1] = (float)L.y;
-  o[2] = (float)L.z;
+// The reference's special values (render.rs:287-292). ray_color returns
+// (attenuation * scattering_pdf * L_sub) / pdf_val, recursively: a bounce whose mixture PDF value
+// is 0 (or NaN) turns the whole sample into inf or NaN per channel, even when the sub-path
+// returns 0 (0 / 0 = NaN) -- something the forward beta/L product cannot see, since nothing may
+// be added after it. Such a bounce sets RT_XS_ON: from then on the lane traces the sub-path with
+// a fresh beta = 1, L = 0, and a channel ends as
+//   NaN  if its bit in RT_XS_NAN is set (c = atten * s_pdf is 0 or NaN there: 0 * x / 0, or the
+//        prefix throughput is 0 or NaN: 0 * inf), or L_sub is 0 or NaN (0 / 0, NaN / 0);
+//   +inf otherwise (x / 0 with x > 0; a later such bounce inside the sub-path resolves the same
+//        way, and the finite radiance gathered before it is absorbed by the inf / NaN).
+// Radiance is never negative (attenuations, emission and PDFs are >= 0), so no -inf arises.
+constexpr uint32_t RT_XS_ON = 8u;
+__device__ __forceinline__ uint32_t xs_nan_bits(d3 c, d3 beta) {
+  const bool nx = !(c.x != 0.0) | !(beta.x != 0.0);  // 0 or NaN
+  const bool ny = !(c.y != 0.0) | !(beta.y != 0.0);
+  const bool nz = !(c.z != 0.0) | !(beta.z != 0.0);
+  return (nx ? 1u : 0u) | (ny ? 2u : 0u) | (nz ? 4u : 0u);
+}
+__device__ __forceinline__ double xs_chan(double l, bool nan_bit) {
+  const double qnan = __builtin_nan("");
+  return (nan_bit | !(l != 0.0)) ? qnan : kInf;  // !(l != 0): 0 or NaN
+}
+__device__ __forceinline__ d3 xs_resolve(d3 L, uint32_t xs) {
+  if (!(xs & RT_XS_ON)) return L;
+  return mk(xs_chan(L.x, xs & 1u), xs_chan(L.y, xs & 2u), xs_chan(L.z, xs & 4u));
 }
 
 // ---------------------------------------------------------------- the path kernel
@@ -1302,45 +1327,86 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   do {          \
   } while (0)
 #endif
-  // Persistent waves: a wave takes pools (one 8x8 tile x one stratum row s_j: nv * sqrt_spp
-  // paths) from a global queue and its lanes claim paths across pool boundaries, so lanes only
-  // idle at the very end of the launch. Wave-uniform pool state:
+  // Persistent waves over a global pool queue. A pool is a (tile, s_j) pair of
+  // one 8x8 pixel tile and one stratum row s_j, or a block of kPoolSi stratum columns of one:
+  //  * row pools (pairs [0, n_pairs_a)): one item per pixel = the whole stratum row (pixel, s_j);
+  //    the lane traces its sqrt_spp samples in the reference's s_i order (render.rs:185-189) and
+  //    keeps their f64 running sum in LDS, then writes ONE f64 RGB partial per (pixel, s_j);
+  //  * tail pools (the last pairs, per s_i block): one item per pixel-sample, written as f64 RGB
+  //    to its own output value; rt_reduce sums a tail pair's samples in s_i order, which is the
+  //    running sum a row item computes, bit for bit. The tail keeps lanes busy while the last
+  //    rows finish, so the launch ends within a few paths per lane.
+  // Idle lanes claim the next item of the wave's pool (ballot + mbcnt), across pool boundaries,
+  // so lanes only idle at the very end of the launch. Wave-uniform pool state:
   const int lane = threadIdx.x & 63;
-  // pool = (tile, s_j, block of kPoolSi stratum columns s_i); tsj = tile * n_sj + s_j index
-  int tsj = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_j = 0;
-  bool more = true;  // the queue may still hold pools
+  int q = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_jp = 0;
+  bool tailp = false;  // the pool is a tail pool (one item per sample)
+  uint32_t out0 = 0;   // tail pools: output index of (s_i = 0, pv = 0)
+  bool more = true;    // the queue may still hold pools
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
+  constexpr int NB = BlockOf<BVH>::value;
+  // per-lane f64 running sum of the item in flight (row items: the stratum row so far)
+  __shared__ double sh_acc[3 * NB];
+  const int tid = threadIdx.x;
 
   d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
   double tm = 0.;
   int depth = 0;
-  bool alive = false;
-  size_t slot = 0;  // per-sample output slot of the path in flight
-  int next = 0;     // pool items claimed so far (wave-uniform)
+  bool alive = false;  // a path is in flight
+  bool fresh = false;  // the lane's next sample needs its camera ray (claimed item / next s_i)
+  uint32_t xk = 0;     // x | row-in-call << 16 | tail item << 31
+  uint32_t sij = 0;    // s_j << 16 | s_i of the sample in flight
+  uint32_t outi = 0;   // output index of the item (TraceParams::part)
+  uint32_t xs = 0;     // special-value state of the path (RT_XS_*)
+  int next = 0;        // pool items claimed so far (wave-uniform)
   Rng g = {0u, 0u, 0u, 0u};
+  // A sample's radiance is final: add it to the item's running sum; a row item continues with
+  // its next s_i, a finished item writes its f64 sum.
+  auto end_sample = [&](d3 L) {
+    L = xs_resolve(L, xs);
+    double a0 = sh_acc[tid] + L.x, a1 = sh_acc[NB + tid] + L.y, a2 = sh_acc[2 * NB + tid] + L.z;
+    alive = false;
+    if (!(xk >> 31) && (int)(sij & 0xffffu) + 1 < P.sqrt_spp) {
+      sh_acc[tid] = a0, sh_acc[NB + tid] = a1, sh_acc[2 * NB + tid] = a2;
+      sij += 1u;
+      fresh = true;
+    } else {
+      double* o = P.part + (size_t)outi * 3;
+      o[0] = a0, o[1] = a1, o[2] = a2;
+    }
+  };
 
   for (;;) {
     PROF(0);
     // ---- pool scheduling: every idle lane claims the next unclaimed item (all 64 lanes are
     // active here: lanes only ever leave the loop together)
-    const bool idle = !alive;
+    const bool idle = !alive && !fresh;
     const unsigned long long want = __ballot(idle);
     if (want != 0ull && next >= pool && more) {  // current pool drained: take the next one
       uint32_t id = 0u;
       if (lane == 0) id = atomicAdd(P.queue, 1u);
       id = __builtin_amdgcn_readfirstlane(id);
       if ((int)id < P.n_pools) {
-        const int blk = (int)id % P.n_blk;
-        tsj = (int)id / P.n_blk;
-        const int tile = tsj / P.n_sj;
+        int blk = 0;
+        tailp = (int)id >= P.n_pairs_a;
+        if (tailp) {
+          const int b = (int)id - P.n_pairs_a;
+          const int qb = b / P.n_blk;
+          blk = b - qb * P.n_blk;
+          q = P.n_pairs_a + qb;
+          out0 = (uint32_t)P.n_pairs_a * 64u + (uint32_t)qb * (uint32_t)P.sqrt_spp * 64u;
+        } else {
+          q = (int)id;
+        }
+        const int tile = q / P.n_sj;
         tx = tile % P.tiles_x;
         ty = tile / P.tiles_x;
         tile_w = imin(kWaveTile, P.W - tx * kWaveTile);
         nv = tile_w * imin(kWaveTile, P.n_rows - ty * kWaveTile);
         si0 = blk * kPoolSi;
-        pool = nv * imin(kPoolSi, P.sqrt_spp - si0);
-        s_j = P.sj0 + tsj % P.n_sj;
+        pool = tailp ? nv * imin(kPoolSi, P.sqrt_spp - si0) : nv;
+        s_jp = P.sj0 + (q - tile * P.n_sj);
       } else {
         more = false;
         pool = 0;
@@ -1352,63 +1418,60 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
           (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
       const int k = next + rank;
       if (k < pool) {
-        int pv, s_i, px_, py_;
+        int pv, s_i;
         if (nv == kWaveTile * kWaveTile) {  // full tile (wave-uniform): shifts
           pv = k & (kWaveTile * kWaveTile - 1);
           s_i = si0 + (k >> 6);
-          px_ = pv & (kWaveTile - 1);
-          py_ = pv >> 3;
         } else {
           pv = k % nv;
           s_i = si0 + k / nv;
-          px_ = pv % tile_w;
-          py_ = pv / tile_w;
         }
-        const kparams_t Q = kparams();
-        const int x = tx * kWaveTile + px_;
-        const int kr = ty * kWaveTile + py_;
-        const int y = Q->row_begin + kr * Q->row_step;
-        // slot order of (tile, s_j): s_i * nv + pv (rt_reduce), whatever the s_i block
-        slot = (size_t)tsj * (size_t)(kWaveTile * kWaveTile) * P.sqrt_spp + (size_t)(s_i * nv + pv);
-        // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
-        g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
-                     (uint32_t)(s_j * Q->sqrt_spp + s_i));
-#ifdef RT_ABL_SEED2  // ablation build: the per-sample RNG seeding (pcg4d) done twice
-        {
-          uint32_t xx = (uint32_t)x;
-          asm volatile("" : "+v"(xx));
-          const Rng g2 = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + (int)xx),
-                                  (uint32_t)(s_j * Q->sqrt_spp + s_i));
-          asm volatile("" ::"v"(g2.s0), "v"(g2.s1), "v"(g2.s2), "v"(g2.s3));
-        }
-#endif
-        C.inc(RT_OP_SAMPLES);
-        d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
-        double px = fma(Q->rs, (double)s_i + rnd(g), -0.5);
-        double py = fma(Q->rs, (double)s_j + rnd(g), -0.5);
-        d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
-        d3 origin = karr3(Q->center);
-        if (Q->defocus) {
-          for (;;) {
-            double dx = rnd_pm1(g);
-            double dy = rnd_pm1(g);
-            if (fma(dx, dx, dy * dy) < 1.0) {
-              const kparams_t R = kparams();
-              origin = vfma(dy, karr3(R->ddv), vfma(dx, karr3(R->ddu), karr3(R->center)));
-              break;
-            }
-          }
-        }
-        ro = origin;
-        rd = ps - origin;
-        tm = rnd(g);
-        beta = mk(1., 1., 1.);
-        Lp = mk(0., 0., 0.);
-        depth = P.max_depth;
-        alive = true;
+        if (!tailp) s_i = 0;
+        const int x = tx * kWaveTile + pv % tile_w;
+        const int kr = ty * kWaveTile + pv / tile_w;
+        xk = (uint32_t)x | (uint32_t)kr << 16 | (tailp ? 0x80000000u : 0u);
+        sij = (uint32_t)s_jp << 16 | (uint32_t)s_i;
+        outi = tailp ? out0 + (uint32_t)s_i * 64u + (uint32_t)pv : (uint32_t)q * 64u + (uint32_t)pv;
+        sh_acc[tid] = 0.0, sh_acc[NB + tid] = 0.0, sh_acc[2 * NB + tid] = 0.0;
+        fresh = true;
       }
     }
     next += __popcll(want);
+    if (fresh) {
+      const kparams_t Q = kparams();
+      const int x = (int)(xk & 0xffffu);
+      const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
+      const int s_i = (int)(sij & 0xffffu), s_j = (int)(sij >> 16);
+      // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
+      g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
+                   (uint32_t)(s_j * Q->sqrt_spp + s_i));
+      C.inc(RT_OP_SAMPLES);
+      d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
+      double px = fma(Q->rs, (double)s_i + rnd(g), -0.5);
+      double py = fma(Q->rs, (double)s_j + rnd(g), -0.5);
+      d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
+      d3 origin = karr3(Q->center);
+      if (Q->defocus) {
+        for (;;) {
+          double dx = rnd_pm1(g);
+          double dy = rnd_pm1(g);
+          if (fma(dx, dx, dy * dy) < 1.0) {
+            const kparams_t R = kparams();
+            origin = vfma(dy, karr3(R->ddv), vfma(dx, karr3(R->ddu), karr3(R->center)));
+            break;
+          }
+        }
+      }
+      ro = origin;
+      rd = ps - origin;
+      tm = rnd(g);
+      beta = mk(1., 1., 1.);
+      Lp = mk(0., 0., 0.);
+      depth = P.max_depth;
+      xs = 0u;
+      alive = true;
+      fresh = false;
+    }
     if (__ballot(alive) == 0ull) {
       if (!more) break;
       continue;
@@ -1416,8 +1479,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (!alive) continue;
     if (depth <= 0) {  // ray_color depth guard render.rs:260-262
       C.inc(RT_OP_DEPTH_CUTOFF);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
+      end_sample(Lp);
       continue;
     }
     C.inc(RT_OP_WORLD_QUERIES);
@@ -1446,8 +1508,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * karr3(kparams()->bg);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
+      end_sample(Lp);
       continue;
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
@@ -1504,8 +1565,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
-      store_sample(P.samp, slot, Lp);
-      alive = false;
+      end_sample(Lp);
       continue;
     }
     if (kind == RT_MAT_METAL) {  // material.rs:124-134
@@ -1641,6 +1701,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 #endif
       PROF(6);
       factor = atten * (s_pdf * rcp_w(pdf_val));
+      if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
+        xs |= RT_XS_ON | xs_nan_bits(atten * s_pdf, beta);
+        Lp = mk(0., 0., 0.);
+        beta = mk(1., 1., 1.);
+        factor = beta;
+      }
     }
     if (diel) {
       // reflect (vec3.rs:219-221) or refract (vec3.rs:223-229; its cos_theta is cos_t)

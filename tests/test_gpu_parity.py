@@ -26,7 +26,7 @@ def _gpu(blob, cam, **kw):
     return acc, st
 
 
-def _compare(blob, cam, seed=1, flags=rt.RT_FLAG_OVERWRITE, check_ops=True, **kw):
+def _compare(blob, cam, seed=1, flags=rt.RT_FLAG_OVERWRITE, check_ops=True, ops_rtol=0.0, **kw):
     acc_g, st = _gpu(blob, cam, seed=seed, flags=flags | rt.RT_FLAG_COUNT_OPS, **kw)
     # the product kernels (no op counters) take shortcuts the counting build does not: span-1
     # BVH leaves are tested once (RTL_DUP), ConstantMedium boundaries are queried in one walk
@@ -41,15 +41,27 @@ def _compare(blob, cam, seed=1, flags=rt.RT_FLAG_OVERWRITE, check_ops=True, **kw
         f"scene-specialised vs interpreter kernel: max |d| {np.nanmax(np.abs(acc_p - acc_i))}"
     opts = rt.make_opts(cam, seed=seed, flags=flags, **kw)
     acc_o, ops_o = O.render(blob, cam, opts, precision=64)
-    spp = cam.samples_per_pixel
-    diff = np.abs(acc_g.astype(np.float64) - acc_o.astype(np.float64)) / spp
-    assert np.isfinite(acc_g).all() == np.isfinite(acc_o).all()
-    fin = np.isfinite(diff)
-    assert diff[fin].max() <= TOL, f"max |d| = {diff[fin].max()} at {np.unravel_index(np.argmax(np.where(fin, diff, 0)), diff.shape)}"
+    _check_values(acc_g, acc_o, cam, kw.get("sj_count", 0))
     if check_ops:
         ops_g = st.op_counts()
-        assert ops_g == ops_o, {k: (ops_g[k], ops_o[k]) for k in ops_o if ops_g[k] != ops_o[k]}
+        bad = {k: (ops_g[k], ops_o[k]) for k in ops_o
+               if abs(ops_g[k] - ops_o[k]) > ops_rtol * max(ops_g[k], ops_o[k])}
+        assert not bad, bad
     return acc_g, acc_o, st
+
+
+def _check_values(acc_g, acc_o, cam, sj_count=0):
+    """Per pixel and channel: the same NaN / +-inf positions as the oracle (the reference's
+    special values, render.rs:287-292), and finite values within TOL of the oracle's per-sample
+    average."""
+    spp = cam.sqrt_spp * (sj_count or cam.sqrt_spp)
+    assert np.array_equal(np.isnan(acc_g), np.isnan(acc_o)), \
+        f"NaN masks differ at {np.argwhere(np.isnan(acc_g) != np.isnan(acc_o))[:8].tolist()}"
+    assert np.array_equal(np.isposinf(acc_g), np.isposinf(acc_o)), "+inf masks differ"
+    assert np.array_equal(np.isneginf(acc_g), np.isneginf(acc_o)), "-inf masks differ"
+    fin = np.isfinite(acc_g)
+    diff = np.abs(acc_g[fin].astype(np.float64) - acc_o[fin].astype(np.float64)) / spp
+    assert diff.size == 0 or diff.max() <= TOL, f"max |d| = {diff.max()}"
 
 
 def test_device_present(gpu_available):
@@ -219,8 +231,9 @@ def test_jit_kernel_runs_for_cornell(gpu_available):
     blob, cam = rt.preset_blob("cornell_smoke", width=48, spp=4)
     assert _jit_state(blob, cam)[0] == 1  # ConstantMedium records call volume_hit
     blob, cam = rt.preset_blob("final_scene", width=32, spp=1, depth=4)
-    # BVH scenes: generated walker opt-in (RT_JIT_BVH=1, rt_device.hip), interpreter by default
-    assert _jit_state(blob, cam)[0] == 0
+    # BVH scenes: BVH subtree records call the per-lane walker from the generated top level
+    state, msg = _jit_state(blob, cam)
+    assert state == 1, msg
 
 
 def test_jit_general_quads_moving_spheres_nested_transforms(gpu_available):
@@ -359,3 +372,129 @@ def test_trace_kernel_timing_history(gpu_available):
     for t, st in zip(ms, sts):
         assert 0.0 < t <= st.ms_kernel + 1e-3
     assert ds.trace_ms(2) == ms[1:]
+
+
+# ---------------------------------------------------------------- BASELINE configs at their own
+# settings (width, spp, depth), on row subsets the oracle finishes in seconds
+@pytest.mark.parametrize("cfg,name,kw,rows,ops_rtol", [
+    ("C2", "cornell_box", dict(width=800, spp=1000), (3, 50, 16), 0.0),
+    ("C3", "cornell_smoke", dict(width=800, spp=1000, depth=10), (7, 50, 16), 0.0),
+    ("C4", "final_scene", dict(width=800, spp=5000, depth=40), (250, 310, 2), 1e-4),
+])
+def test_baseline_config_rows_vs_oracle(gpu_available, cfg, name, kw, rows, ops_rtol):
+    """C2/C3 with all 961 spp and C4 with all 4900 spp at depth 40 (main.rs:726): rows
+    row_begin + k * row_step of the 800x800 frame, HIP vs oracle per pixel (values within TOL,
+    NaN / inf positions identical) and op counts.
+
+    Op counts: C2 and C3 take identical paths on both sides. C4's 7.8 M paths of up to 40
+    bounces (Perlin turbulence, 1000-sphere cluster, metal fuzz, fog draws) are not all
+    identical: the device rounds geometry with fma / Newton reciprocals and the oracle follows
+    the reference's plain IEEE order, so a decision taken within an ulp of its threshold (a
+    Schlick draw, an edge hit, a free-flight distance) can go the other way. Measured: ~1.4e-5
+    of the AABB tests and ~4e-6 of the volume tests; the counts must agree within 1e-4."""
+    blob, cam = rt.preset_blob(name, **kw)
+    assert cam.image_width == 800 and cam.image_height == 800
+    b, s_, n = rows
+    acc_g, acc_o, st = _compare(blob, cam, row_begin=b, row_step=s_, n_rows=n, ops_rtol=ops_rtol)
+    assert st.samples == n * 800 * cam.samples_per_pixel
+
+
+def test_c5_camera_rows_vs_oracle(gpu_available):
+    """C5 (book3 Cornell scene at 16:9, 3840x2160, 10000 spp, depth 50): the wide camera on two
+    rows and a stratum subset (s_j 40..42 of 100: full-spp jitter, 300 samples per pixel)."""
+    blob, cam = rt.preset_blob("cornell_box", width=3840, spp=10000, aspect=16.0 / 9.0)
+    assert (cam.image_width, cam.image_height, cam.sqrt_spp) == (3840, 2160, 100)
+    _compare(blob, cam, row_begin=700, row_step=700, n_rows=2, sj_begin=40, sj_count=3)
+
+
+def _render_env(blob, cam, env, **kw):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return _gpu(blob, cam, **kw)[0]
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("cornell_box", dict(width=96, spp=100)),
+    ("final_scene", dict(width=64, spp=16, depth=40)),
+])
+def test_chunked_and_tail_split_renders_are_bitwise_equal(gpu_available, name, kw):
+    """The stratum-row chunk loop (RT_WORKSPACE_MB too small for one launch: several launches
+    carry the f64 running sums across rt_reduce calls) and the split between row items and
+    per-sample tail items (RT_TAIL_PAIRS) leave the image bit for bit unchanged."""
+    blob, cam = rt.preset_blob(name, **kw)
+    one = _render_env(blob, cam, {})
+    for env in ({"RT_WORKSPACE_MB": 1}, {"RT_TAIL_PAIRS": 0}, {"RT_TAIL_PAIRS": 1 << 30},
+                {"RT_TAIL_PAIRS": 7, "RT_WORKSPACE_MB": 1}):
+        other = _render_env(blob, cam, env)
+        assert np.array_equal(one, other, equal_nan=True), env
+
+
+def _zero_pdf_scene():
+    """A floor whose light-sampled bounces have pdf_val = 0 exactly, and whose sub-paths then
+    return 0. The light list holds a quad 1e-9 below the floor's plane (not in the world): a
+    direction sampled towards it from the floor has |n.d| ~ 1e-9 < 1e-8, so Quad::pdf_value
+    misses (object.rs:457, 492-501), the top light misses too, and the direction points
+    (robustly, 1e-9 >> rounding) below the floor, so the cosine PDF and scattering_pdf are 0.
+    The sub-path runs nearly horizontally into a wall whose BACK face is a DiffuseLight:
+    emitted = 0 and no scatter (material.rs:210-222), so L = 0 and the reference computes
+    (attenuation * 0 * 0) / 0 = NaN (render.rs:289-290) for the whole sample."""
+    sc = rt.Scene(9)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    light = sc.diffuse_light((6, 6, 6))
+    floor = sc.quad((-4, 0, -4), (8, 0, 0), (0, 0, 8), white)
+    top = sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light)
+    walls = [sc.quad((6, -1, -6), (0, 4, 0), (0, 0, 12), light),    # normals point outwards:
+             sc.quad((-6, -1, -6), (0, 0, 12), (0, 4, 0), light),   # rays from inside see
+             sc.quad((-6, -1, 6), (0, 4, 0), (12, 0, 0), light),    # their back faces
+             sc.quad((-6, -1, -6), (12, 0, 0), (0, 4, 0), light)]
+    world = sc.hittable_list(floor, top, sc.sphere((0, 1, 0), 1.0, white), *walls)
+    lights = sc.hittable_list(sc.quad((4.5, -1e-9, -1), (1, 0, 0), (0, 0, 2), light),
+                              sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 48, 16, 10, 60, (0, 3, 5), (0, 0.5, 0), (0, 1, 0), 0, 0, (0, 0, 0))
+    return blob, cam
+
+
+def test_zero_pdf_bounce_nan_semantics(gpu_available):
+    """render.rs:287-292: a bounce with pdf_val = 0 makes the sample NaN even when its sub-path
+    returns 0 (_zero_pdf_scene). The forward beta/L product alone would leave those samples
+    finite (nothing is added after the bounce); the HIP path must put NaN in exactly the
+    oracle's pixels and channels."""
+    blob, cam = _zero_pdf_scene()
+    acc_g, acc_o, _ = _compare(blob, cam)
+    assert np.isnan(acc_g).mean() > 0.2 and np.isfinite(acc_g).any()
+
+
+def test_black_pixels_of_the_600_cornell_camera(gpu_available):
+    """book3.png's all-black pixels (31,671; tests/golden/final_images_stats.json). The count is
+    not exact by construction: a pixel whose corner is clipped by the box opening is black only
+    if every jittered sample misses, which depends on the reference's unseeded draws, and a
+    pixel seeing dark geometry maps to 0 below sRGB8 0.5 (color.rs:30). The HIP render and the
+    oracle must agree EXACTLY (same seed), and both within 0.2 % of the published count."""
+    import json
+    from pathlib import Path
+
+    ref = json.loads((Path(__file__).parent / "golden" / "final_images_stats.json").read_text())
+    m = ref["book3.png"]
+    blob, cam = rt.preset_blob(m["preset"], variant=m["variant"], width=m["width"],
+                               spp=m["spp"], depth=m["depth"])
+    rows = (0, 37, 17)  # 17 rows through the top, the box and the floor
+    acc_g, _ = _gpu(blob, cam, seed=1, row_begin=rows[0], row_step=rows[1], n_rows=rows[2])
+    acc_o, _ = O.render(blob, cam, rt.make_opts(cam, seed=1, row_begin=rows[0], row_step=rows[1],
+                                                n_rows=rows[2]), precision=64)
+    rgb_g = rt.write_color(acc_g, cam.samples_per_pixel)
+    rgb_o = rt.write_color(acc_o, cam.samples_per_pixel)
+    black_g = rgb_g.reshape(-1, 3).sum(1) == 0
+    assert np.array_equal(black_g, rgb_o.reshape(-1, 3).sum(1) == 0)
+    full, _ = _gpu(blob, cam, seed=1)
+    black = int((rt.write_color(full, cam.samples_per_pixel).reshape(-1, 3).sum(1) == 0).sum())
+    print(f"black pixels: {black} (book3.png: {m['black_pixels']})")
+    assert abs(black - m["black_pixels"]) <= 0.002 * m["black_pixels"], black
