@@ -15,7 +15,10 @@ Also reported (one JSON line on rank 0):
                kernel's average duration (HIP events recorded by the library around each
                rt_trace launch on the bench stream, rt_scene_trace_ms), vs 78.6 TF; render_ms =
                the whole render call (rt_trace + rt_reduce, torch.cuda.Event on that stream).
-  scene_fetch  the north star's "HBM GB/s on BVH traversal": logical scene-record bytes / time.
+  hbm          the north star's "achieved HBM GB/s" of the path kernel (BVH traversal at C4):
+               rocprofv3 PMC FETCH_SIZE + WRITE_SIZE bytes per rt_trace launch, from the committed
+               profile of this exact workload (profiles/pmc_traffic_<config>.json; PMC counters
+               cannot be read inside this process), over this run's kernel time, vs 8 TB/s.
   cpu_baseline the f64 CPU oracle (a restatement of the reference; the Rust original cannot be
                built here) on this host's cores, timed on a bounded stratum subset of the same
                frame (rank 0, N = 1 only).
@@ -153,6 +156,10 @@ def main():
         st = ds.render_device(cam, copts, local_buf.data_ptr(), stream.cuda_stream, stats=True)
         ops = st.op_counts()
 
+    # one product render with stats (outside the timed region): the bytes the path kernel
+    # stores per launch (f64 row partials + tail samples) = its algorithmic HBM bytes
+    pst = ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream, stats=True)
+    out_bytes_launch = pst.out_bytes / max(1, pst.launches)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -208,35 +215,46 @@ def main():
             },
         }
         if ops is not None:
-            # flops / bytes of the rank-0 launch (its share of rows) over its kernel time
+            # flops of the rank-0 launch (its share of rows) over its kernel time; kernel_ms is
+            # per render, i.e. summed over the render's launches (stratum-row chunks)
             fl = roofline.flops(ops)
-            by = roofline.scene_bytes(ops, partial_bytes=n * W * spp * 24)  # sample slots w+r
             ach = fl / (kernel_ms * 1e-3) / 1e12
             # PMC HBM bytes per rt_trace launch, measured by tools_gpu/profile_round.sh at N = 1
             # for this exact workload (null otherwise: a rank's launch at N > 1 is a different size)
-            traffic = None
+            prof = None
             tf = REPO / "profiles" / f"pmc_traffic_{args.config}.json"
             if world == 1 and args.config_name != "custom" and tf.exists():
                 try:
-                    traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+                    prof = json.loads(tf.read_text())
                 except Exception:
-                    traffic = None
+                    prof = None
+            traffic = prof.get("hbm_bytes_per_launch") if prof else None
             res["roofline"] = {
                 "bound": "valu", "achieved": round(ach, 3),
                 "peak": roofline.PEAK_FP64_VECTOR_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / roofline.PEAK_FP64_VECTOR_TFLOPS, 4),
                 "traffic": traffic,
+                "traffic_source": (f"profiles/{tf.name} (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
+                                   "passes of this workload, per rt_trace launch; not this run)"
+                                   if traffic is not None else None),
                 "kernel": "rt_trace", "kernel_ms": round(kernel_ms, 3),
+                "launches_per_render": pst.launches,
                 "render_ms": round(step_gpu_ms, 3),
-                "flops_per_launch": fl, "flops_per_sample": round(fl / ops["samples"], 1),
+                "flops_per_launch": fl / max(1, pst.launches),
+                "flops_per_sample": round(fl / ops["samples"], 1),
+                "algorithmic_bytes_per_launch": out_bytes_launch,
             }
-            gbps = by / (kernel_ms * 1e-3) / 1e9
-            res["scene_fetch"] = {
-                "achieved": round(gbps, 1), "peak": roofline.PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": round(gbps / roofline.PEAK_HBM_GBPS, 4),
-                "bytes_per_launch": by,
-                "note": "logical scene-record bytes (L1/L2-resident), not HBM traffic",
-            }
+            if traffic is not None:
+                launch_s = kernel_ms * 1e-3 / max(1, pst.launches)
+                res["hbm"] = {
+                    "achieved": round(traffic / launch_s / 1e9, 2),
+                    "peak": roofline.PEAK_HBM_GBPS, "unit": "GB/s",
+                    "frac": round(traffic / launch_s / 1e9 / roofline.PEAK_HBM_GBPS, 5),
+                    "fetch_bytes_per_launch": prof.get("fetch_bytes"),
+                    "write_bytes_per_launch": prof.get("write_bytes"),
+                    "note": "measured PMC bytes (profile above) / this run's rt_trace time; the "
+                            "kernel is FP64-VALU bound, HBM is not its roof",
+                }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(blob, cam, args.seed, args.cpu_seconds)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)

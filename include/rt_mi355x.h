@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define RT_OK 0
@@ -185,6 +185,10 @@ typedef struct rt_stats {
   double ms_total;   /* host wall time of the call                                  */
   uint64_t samples;  /* pixel-samples rendered by this call                         */
   uint64_t ops[32];  /* rt_op_counter values (RT_FLAG_COUNT_OPS only)               */
+  uint64_t out_bytes; /* f64 partial / tail-sample bytes the path kernel stored (and   */
+                      /* rt_reduce read back): the algorithmic HBM bytes of the render  */
+  uint32_t launches;  /* path-kernel launches (stratum-row chunks) of the render        */
+  uint32_t _pad0;
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque: device-resident flattened scene + workspace */

@@ -595,8 +595,12 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.part = (double*)(sc->work + tot_bytes);
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
+  uint64_t out_bytes = 0;
+  uint32_t launches = 0;
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
     const int cn = std::min(chunk, sj0 + n_sj - c0);
+    out_bytes += part_bytes(cn);
+    ++launches;
     const int64_t pairs = (int64_t)n_tiles * cn;
     const int64_t tb = std::min<int64_t>(pairs, tail);
     P.sj0 = c0;
@@ -633,6 +637,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     HIP_TRY(hipEventElapsedTime(&ms, sc->ev0, sc->ev1));
     stats->ms_kernel = ms;
     stats->samples = (uint64_t)n_px * (uint64_t)n_sj * (uint64_t)S;
+    stats->out_bytes = out_bytes;
+    stats->launches = launches;
     if (count) {
       unsigned long long h[32];
       HIP_TRY(hipMemcpy(h, sc->ops, sizeof(h), hipMemcpyDeviceToHost));

@@ -513,6 +513,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_HIT2
   opts.push_back("-DRT_ABL_HIT2");
 #endif
+#ifdef RT_ABL_NOXS
+  opts.push_back("-DRT_ABL_NOXS");
+#endif
 #ifdef RT_ABL_SEED2
   opts.push_back("-DRT_ABL_SEED2");
 #endif

@@ -1477,10 +1477,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       continue;
     }
     if (!alive) continue;
+    // One bounce. `break` leaves the block: the path bounced (metal) or ended (term: depth
+    // cut-off, miss, light); the ending lanes of all three kinds then share ONE end_sample.
+    bool term = false;
+    do {
     if (depth <= 0) {  // ray_color depth guard render.rs:260-262
       C.inc(RT_OP_DEPTH_CUTOFF);
-      end_sample(Lp);
-      continue;
+      term = true;
+      break;
     }
     C.inc(RT_OP_WORLD_QUERIES);
     PROF(1);
@@ -1508,8 +1512,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       Lp = Lp + beta * karr3(kparams()->bg);
-      end_sample(Lp);
-      continue;
+      term = true;
+      break;
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
     PROF(2);
@@ -1565,8 +1569,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
-      end_sample(Lp);
-      continue;
+      term = true;
+      break;
     }
     if (kind == RT_MAT_METAL) {  // material.rs:124-134
       C.inc(RT_OP_METAL);
@@ -1577,7 +1581,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       ro = p;
       rd = reflected;
       --depth;
-      continue;
+      break;
     }
     // Dielectric (material.rs:166-191), Lambertian and Isotropic (the mixture-PDF branch,
     // render.rs:278-292) run as ONE block: a wave holding both kinds of lanes shares the unit
@@ -1701,12 +1705,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 #endif
       PROF(6);
       factor = atten * (s_pdf * rcp_w(pdf_val));
+#ifndef RT_ABL_NOXS  // ablation build: no special-value tracking (cost of RT_XS_*)
       if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
         xs |= RT_XS_ON | xs_nan_bits(atten * s_pdf, beta);
         Lp = mk(0., 0., 0.);
         beta = mk(1., 1., 1.);
         factor = beta;
       }
+#endif
     }
     if (diel) {
       // reflect (vec3.rs:219-221) or refract (vec3.rs:223-229; its cos_theta is cos_t)
@@ -1719,6 +1725,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     ro = p;
     rd = dir;
     --depth;
+    } while (false);
+    if (term) end_sample(Lp);
   }
 #ifdef RT_PROF
   PROF(7);

@@ -74,7 +74,8 @@ class RtRenderOpts(C.Structure):
 
 class RtStats(C.Structure):
     _fields_ = [("ms_kernel", C.c_double), ("ms_total", C.c_double), ("samples", C.c_uint64),
-                ("ops", C.c_uint64 * 32)]
+                ("ops", C.c_uint64 * 32), ("out_bytes", C.c_uint64), ("launches", C.c_uint32),
+                ("_pad0", C.c_uint32)]
 
     def op_counts(self) -> dict:
         return {n: int(self.ops[i]) for i, n in enumerate(OP_NAMES)}
@@ -196,7 +197,7 @@ def load_device_lib(path: Path) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rt_abi_version() != 1:
+    if lib.rt_abi_version() != 2:
         raise RuntimeError("librtmi355x ABI version mismatch")
     return lib
 

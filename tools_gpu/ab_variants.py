@@ -6,6 +6,8 @@ import os
 import sys
 import time
 
+if os.environ.get("AB_TORCH", "1") == "1":
+    import torch  # noqa: F401  (bench.py imports torch first: its bundled hiprtc builds the kernels)
 sys.path.insert(0, "surely-raytracing_amd")
 import numpy as np  # noqa: E402
 import surely_rt as rt  # noqa: E402
@@ -16,10 +18,17 @@ ROUNDS = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 SCENE = sys.argv[4] if len(sys.argv) > 4 else "cornell_box"
 VARDIR = os.environ.get("VARDIR", "build/variants")
 paths = ["build/librtmi355x.so"] + sorted(glob.glob(f"{VARDIR}/*.so"))
+# AB_ENVS="K=V,K2=V2;K=V3": extra entries rendering with the default library under these
+# environment settings (read by the library at each render call)
+envs = {p: {} for p in paths}
+for spec in filter(None, os.environ.get("AB_ENVS", "").split(";")):
+    key = "build/librtmi355x.so[" + spec + "]"
+    paths.append(key)
+    envs[key] = dict(kv.split("=", 1) for kv in spec.split(","))
 blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
 libs, scenes = [], []
 for p in paths:
-    lib = rt.load_device_lib(p)
+    lib = rt.load_device_lib(p.split("[")[0]) if "[" not in p else libs[0]
     h = C.c_void_p()
     assert lib.rt_scene_create(blob.ref(), 0, C.byref(h)) == 0, lib.rt_last_error()
     libs.append(lib)
@@ -31,7 +40,14 @@ for r in range(ROUNDS + 1):
     for p, lib, h in zip(paths, libs, scenes):
         acc = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
         st = rt.RtStats()
+        saved = {k: os.environ.get(k) for k in envs[p]}
+        os.environ.update(envs[p])
         assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
         if ref is None:
             ref = acc
         same = np.array_equal(acc, ref)

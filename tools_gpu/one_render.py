@@ -1,8 +1,10 @@
 """One render through the C ABI for profiling: python tools_gpu/one_render.py [scene width spp reps]"""
+import os
 import sys
+if os.environ.get("AB_TORCH", "1") == "1":
+    import torch  # noqa: F401  (as bench.py: torch's bundled hiprtc builds the scene kernels)
 sys.path.insert(0, "surely-raytracing_amd")
 import surely_rt as rt  # noqa: E402
-import os  # noqa: E402
 
 if os.environ.get("RT_LIB"):  # profiling a library variant (tools only; the product loads build/)
     rt._dev = rt.load_device_lib(os.environ["RT_LIB"])

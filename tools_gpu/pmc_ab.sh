@@ -11,7 +11,7 @@ for LIB in build/librtmi355x.so $VAR; do
   for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_INSTS_VALU_FMA_F64" \
              "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA"; do
     j=$((j+1))
-    RT_LIB=$LIB timeout -k 10 120 rocprofv3 --pmc $SET --kernel-trace -d $OUT/l$i/p$j -o run --output-format csv -- python3 tools_gpu/one_render.py cornell_box 800 100 > $OUT/l$i/p$j.log 2>&1 || exit $?
+    RT_LIB=$LIB timeout -k 10 120 rocprofv3 --pmc $SET --kernel-trace -d $OUT/l$i/p$j -o run --output-format csv -- python3 tools_gpu/one_render.py ${SCENE:-cornell_box} 800 ${SPP:-1000} > $OUT/l$i/p$j.log 2>&1 || exit $?
   done
   python3 tools_gpu/pmc_summary.py $OUT/l$i > $OUT/summary_l$i.txt 2>&1
 done

@@ -1,19 +1,21 @@
 """Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to per-launch HBM bytes of rt_trace.
 
 MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half the bytes of a 16-B/lane streaming read and
-other access widths are uncalibrated. rt_trace does no streaming reads (scene records come from
-K$/L2; the only bulk traffic is the 12-B per-sample slot stores), so the counters are reported
-raw (KiB -> bytes, no x2), and WRITE_SIZE is calibrated against the known slot bytes of the
-launch (argv[4] = samples per launch x 12 B).
-Usage: pmc_to_json.py OUT.json FETCH_GLOB WRITE_GLOB [ALGORITHMIC_WRITE_BYTES]"""
+other access widths are uncalibrated. rt_trace's reads are scalar scene-record loads (K$/L2),
+per-lane BVH/leaf records and scratch spill reloads, none of them 16-B/lane streaming, so
+FETCH_SIZE is reported raw (KiB -> bytes, no x2). Its stores are the f64 row partials / tail
+samples (24 B per lane-store) plus any scratch spill write-backs, so WRITE_SIZE is calibrated
+per launch against the known output bytes of one launch (argv[4], bench.py's
+algorithmic_bytes_per_launch): write_calibration = 1 means no extra write traffic.
+Usage: pmc_to_json.py OUT.json FETCH_GLOB WRITE_GLOB [ALGORITHMIC_WRITE_BYTES_PER_LAUNCH]"""
 import csv
 import glob
 import json
 import sys
 
 out = sys.argv[1]
-algo_write = float(sys.argv[4]) if len(sys.argv) > 4 else None
-vals = {}
+algo_write = float(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else None
+vals, n = {}, {}
 for name, pat in (("FETCH_SIZE", sys.argv[2]), ("WRITE_SIZE", sys.argv[3])):
     per = []
     for f in glob.glob(pat):
@@ -21,18 +23,21 @@ for name, pat in (("FETCH_SIZE", sys.argv[2]), ("WRITE_SIZE", sys.argv[3])):
             if "rt_trace" in r["Kernel_Name"] and r["Counter_Name"] == name:
                 per.append(float(r["Counter_Value"]))
     vals[name] = sum(per) / max(1, len(per)) if per else None
+    n[name] = len(per)
 fetch, write = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
 fb = fetch * 1024 if fetch is not None else None
 wb = write * 1024 if write is not None else None
 res = {
     "kernel": "rt_trace",
-    "fetch_bytes_raw": fb,
-    "write_bytes_raw": wb,
+    "launches_profiled": n,
+    "fetch_bytes": fb,
+    "write_bytes": wb,
     "hbm_bytes_per_launch": fb + wb if fb is not None and wb is not None else None,
-    "algorithmic_write_bytes": algo_write,
+    "algorithmic_write_bytes_per_launch": algo_write,
     "write_calibration": (wb / algo_write) if wb and algo_write else None,
-    "note": "FETCH_SIZE + WRITE_SIZE per rt_trace launch, raw (no x2: no 16-B streaming reads "
-            "in this kernel); write_calibration = WRITE_SIZE / known per-sample slot bytes",
+    "note": "FETCH_SIZE + WRITE_SIZE (KiB -> B) averaged over the rt_trace launches of the pass, "
+            "raw (no x2: no 16-B streaming reads in this kernel); write_calibration = WRITE_SIZE "
+            "/ the launch's f64 output bytes (1 = no spill / extra write traffic)",
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
