@@ -14,7 +14,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra
 CFLAGS_O := -std=c11 -O2 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
 HOST_SRC := $(CSRC)/host/scene.cpp $(CSRC)/host/presets.cpp $(CSRC)/host/capi.cpp
-DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp $(CSRC)/rt_jit.cpp
+DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp $(CSRC)/rt_obvh.cpp $(CSRC)/rt_jit.cpp
 DEV_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp $(CSRC)/rt_jit.hpp include/rt_mi355x.h $(BUILD)/rt_jit_sources.inc
 JIT_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_layout.h include/rt_mi355x.h $(CSRC)/rt_rng.h
 

@@ -135,6 +135,9 @@ typedef struct rt_camera {
                                            /* Isotropic scattering_pdf = 0 */
 #define RT_FLAG_INTERPRETER 0x8u           /* product render with the interpreter walker, not the */
                                            /* scene-specialised kernel (same image, bit for bit)  */
+#define RT_FLAG_REFERENCE_BVH 0x10u        /* product render walks BVH subtrees in the reference's */
+                                           /* own tree and order, not their ordered BVHs (same    */
+                                           /* image, bit for bit)                                 */
 
 typedef struct rt_render_opts {
   uint64_t seed;      /* render RNG seed                                   */
@@ -200,10 +203,11 @@ int rt_device_count(int* count);
 /* Validate a blob without touching a device (hittable/object invariants, tag and index ranges). */
 int rt_scene_validate(const rt_scene_blob* blob);
 
-/* Host-only diagnostics of the flattened layout (no device needed): out[0..7] = node words,
+/* Host-only diagnostics of the flattened layout (no device needed): out[0..8] = node words,
  * BVH-region words, BVH records, DUP records (span-1 leaves tested once), ConstantMedium
- * records, of which one-walk sphere / one-walk quad boundaries, and light records. */
-#define RT_LAYOUT_STATS 8
+ * records, of which one-walk sphere / one-walk quad boundaries, light records, and BVH
+ * subtrees walked through an ordered BVH by the product kernels. */
+#define RT_LAYOUT_STATS 9
 int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n);
 
 /* Validate, flatten (threaded node array, f64 payloads; rt_layout.h) and upload to `device`. */

@@ -184,10 +184,11 @@ int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n) {
   int rc = rtf::flatten(blob, &F, &err);
   if (rc != RT_OK) return set_err(rc, err);
   uint32_t v[RT_LAYOUT_STATS] = {(uint32_t)F.nodes.size(), F.hdr.bvh_words, 0, 0, 0, 0, 0,
-                                 F.hdr.n_lights};
-  for (size_t p = 0; p < F.nodes.size(); p += rtf::record_words(F.nodes[p])) {
+                                 F.hdr.n_lights, 0};
+  for (size_t p = 0; p < F.hdr.n_rec_words; p += rtf::record_words(F.nodes[p])) {
     const uint32_t h = F.nodes[p], ty = h & 0xffu;
     if (ty == RTL_BVH) ++v[2];
+    if (ty == RTL_BVH && F.nodes[p + 3] != 0u) ++v[8];
     if (ty == RTL_DUP) ++v[3];
     if (ty == RTL_VOLUME) {
       ++v[4];

@@ -9,6 +9,8 @@
 // emitted once per reference, exactly as often as the reference would visit them.
 #include "rt_flatten.hpp"
 
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 
@@ -149,7 +151,19 @@ struct Emitter {
   size_t last_exit_end = (size_t)-1;  // end position of the most recent EXIT node
   size_t last_skip_target = (size_t)-1;
 
+  // conservative bounds of the leaf records emitted (pre-relocation position), for rt_obvh.cpp
+  std::vector<std::pair<size_t, PrimBox>> pbox;
+
   explicit Emitter(std::vector<uint32_t>& words, int64_t nm) : w(words), n_mats(nm) {}
+
+  static void pad_box(PrimBox& b) {
+    for (int k = 0; k < 3; ++k) {
+      const double m = 1e-9 * (1.0 + std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
+      b.lo[k] -= m;
+      b.hi[k] += m;
+    }
+    b.valid = std::isfinite(b.lo[0] + b.lo[1] + b.lo[2] + b.hi[0] + b.hi[1] + b.hi[2]);
+  }
 
   void fail(int code, const std::string& m) {
     if (status == RT_OK) {
@@ -197,6 +211,26 @@ struct Emitter {
       putd(w, p, 16, u[0]), putd(w, p, 17, u[1]), putd(w, p, 18, u[2]);
       putd(w, p, 20, v[0]), putd(w, p, 21, v[1]), putd(w, p, 22, v[2]);
     }
+    if (!light) {  // bounds of the four corners; the reference's Aabb spans q .. q + u + v only
+      PrimBox b;
+      const double q[3] = {f[0], f[1], f[2]};
+      double c[4][3];
+      for (int k = 0; k < 3; ++k) {
+        c[0][k] = q[k], c[1][k] = q[k] + u[k], c[2][k] = q[k] + v[k], c[3][k] = (q[k] + u[k]) + v[k];
+        b.lo[k] = std::min(std::min(c[0][k], c[1][k]), std::min(c[2][k], c[3][k]));
+        b.hi[k] = std::max(std::max(c[0][k], c[1][k]), std::max(c[2][k], c[3][k]));
+      }
+      // Aabb::from_points(q, q + u + v).pad() (object.rs:427, 371-386, interval.rs:43-50)
+      bool complete = true;
+      for (int k = 0; k < 3; ++k) {
+        double lo = std::min(c[0][k], c[3][k]), hi = std::max(c[0][k], c[3][k]);
+        if (hi - lo < 0.0001) lo = lo - 0.0001 / 2., hi = hi + 0.0001 / 2.;
+        for (int m = 1; m < 3; ++m) complete = complete && lo <= c[m][k] && c[m][k] <= hi;
+      }
+      b.ref_complete = complete;
+      pad_box(b);
+      pbox.push_back({p, b});
+    }
     const int ax = light ? RTL_LQUAD_AXIS_D : 0;  // double index of the axis-aligned form
     // axis-aligned fast form (rt_layout.h): only when the exact-zero pattern holds
     auto single = [](const double* x) {
@@ -234,6 +268,18 @@ struct Emitter {
     putd(w, p, 0, f[0]), putd(w, p, 1, f[1]), putd(w, p, 2, f[2]), putd(w, p, 3, f[3]);
     putd(w, p, 4, f[4]), putd(w, p, 5, f[5]), putd(w, p, 6, f[6]);
     putd(w, p, 7, 1.0 / f[3]);  // outward = (p - c) * (1/r)
+    if (!light) {  // c +- r, and at c + cvec when moving (object.rs:88-105)
+      PrimBox b;
+      const double r = std::fabs(f[3]);
+      for (int k = 0; k < 3; ++k) {
+        const double c1 = n.moving ? f[k] + f[4 + k] : f[k];
+        b.lo[k] = std::min(f[k], c1) - r;
+        b.hi[k] = std::max(f[k], c1) + r;
+      }
+      b.ref_complete = true;
+      pad_box(b);
+      pbox.push_back({p, b});
+    }
   }
   // RTL_VOLF_* when the boundary sequence starting at q has the one-walk form (rt_layout.h)
   uint32_t fusable_boundary(size_t q) const {
@@ -284,8 +330,18 @@ struct Emitter {
 #endif
           if (j - i >= 2) {
             size_t p = push(RTL_QUADS | (uint32_t)((j - i) << 8), 4);
+            const size_t first_box = pbox.size();
             for (size_t k = i; k < j; ++k) quad(*n.kids[k], false);
             w[p + 1] = (uint32_t)w.size();
+            PrimBox b = pbox[first_box].second;  // the batch: union of its quads' bounds
+            for (size_t k = first_box + 1; k < pbox.size(); ++k) {
+              const PrimBox& q = pbox[k].second;
+              for (int c = 0; c < 3; ++c)
+                b.lo[c] = std::min(b.lo[c], q.lo[c]), b.hi[c] = std::max(b.hi[c], q.hi[c]);
+              b.valid = b.valid && q.valid;
+              b.ref_complete = b.ref_complete && q.ref_complete;
+            }
+            pbox.push_back({p, b});
             i = j;
           } else {
             emit(*n.kids[i], frame, chain, in_volume);
@@ -389,7 +445,8 @@ namespace {
 // in LDS by rt_trace) and make every link explicit (rt_layout.h): BVH records get their first
 // child in word 2, every other record its pre-order successor in word 3. The visiting order,
 // and with it every result, is unchanged: only the addresses move.
-void relocate(std::vector<uint32_t>& w, uint32_t* root, uint32_t* bvh_words) {
+void relocate(std::vector<uint32_t>& w, uint32_t* root, uint32_t* bvh_words,
+              std::vector<uint32_t>* map_out) {
   std::vector<size_t> pos;
   for (size_t p = 0; p < w.size(); p += record_words(w[p])) pos.push_back(p);
   std::vector<uint32_t> map(w.size() + 1, 0xffffffffu);
@@ -420,6 +477,34 @@ void relocate(std::vector<uint32_t>& w, uint32_t* root, uint32_t* bvh_words) {
   w.swap(out);
   *root = m(*root);
   *bvh_words = nb;
+  map_out->swap(map);
+}
+
+// BVH records where the top-level walk hands a subtree to the per-lane walker (the world
+// sequence and every ConstantMedium boundary sequence, as traverse<UNI> visits them)
+std::vector<uint32_t> bvh_roots(const std::vector<uint32_t>& w, uint32_t root) {
+  std::vector<uint32_t> roots, todo{root};
+  size_t guard = 0;
+  while (!todo.empty()) {
+    uint32_t x = todo.back();
+    todo.pop_back();
+    while (x < w.size() && ++guard < (1u << 26)) {
+      const uint32_t ty = w[x] & 0xffu;
+      if (ty == RTL_END) break;
+      if (ty == RTL_BVH) {
+        roots.push_back(x);
+        x = w[x + 1];
+      } else if (ty == RTL_VOLUME) {
+        todo.push_back(w[x + 3]);  // the boundary sequence
+        x = w[x + 1];
+      } else if (ty == RTL_QUADS || ty == RTL_DUP || ty == RTL_OTHER) {
+        x = w[x + 1];
+      } else {
+        x = w[x + 3];  // QUAD, SPHERE: next; TRANSLATE / ROTATE_Y: child; EXIT: next
+      }
+    }
+  }
+  return roots;
 }
 
 }  // namespace
@@ -595,7 +680,15 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
     return em.status;
   }
   uint32_t root = 0, bvh_words = 0;
-  relocate(F.nodes, &root, &bvh_words);
+  std::vector<uint32_t> map;
+  relocate(F.nodes, &root, &bvh_words, &map);
+  const uint32_t rec_words = (uint32_t)F.nodes.size();
+  {  // ordered BVHs of the product kernels (rt_obvh.cpp), appended after the records
+    std::vector<PrimBox> boxes(rec_words);
+    for (auto& pb : em.pbox)
+      if (pb.first < map.size() && map[pb.first] < rec_words) boxes[map[pb.first]] = pb.second;
+    build_ordered_bvhs(F.nodes, rec_words, boxes, bvh_roots(F.nodes, root));
+  }
   if (F.nodes.size() >= 0x7fffffffu) {
     *err = "scene too large";
     return RT_ERR_UNSUPPORTED;
@@ -639,6 +732,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.root = root;
   h.bvh_words = bvh_words;
   h.n_node_words = (uint32_t)F.nodes.size();
+  h.n_rec_words = rec_words;
   h.n_mats = (uint32_t)n_mat;
   h.n_texs = (uint32_t)n_tex;
   h.n_perlins = (uint32_t)n_perl;

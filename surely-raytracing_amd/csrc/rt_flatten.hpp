@@ -21,6 +21,19 @@ struct FlatScene {
   std::vector<uint8_t> texels;
 };
 
+// Conservative bounds of a leaf record (QUAD, QUADS batch, SPHERE), by record word position.
+// ref_complete: the reference's own Aabb of the primitive (object.rs:427-431: q and q + u + v,
+// padded) contains the whole primitive, so its BVH culls no true candidate.
+struct PrimBox {
+  double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  bool valid = false, ref_complete = false;
+};
+
+// rt_obvh.cpp: append an ordered BVH (rt_layout.h OBVH) for every eligible BVH subtree root in
+// `roots` (word positions of BVH records) and link it from the root's word 3.
+void build_ordered_bvhs(std::vector<uint32_t>& nodes, uint32_t rec_words,
+                        const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots);
+
 // Words of the node record starting with header word h (rt_layout.h).
 uint32_t record_words(uint32_t h);
 

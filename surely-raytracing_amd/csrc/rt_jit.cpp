@@ -373,8 +373,8 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
     } else if (ty == RTL_BVH) {
       // BvhNode subtree [node, skip) per lane (rt_kernel.h traverse<UNI> RTL_BVH)
       o << "    if (BVH) {\n      double tb;\n      uint32_t bn = 0u;\n      int bf = -1;\n"
-        << "      const bool sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, "
-        << N[node + 1] << "u, ro, rd, tm, o, d, " << frame
+        << "      const bool sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, "
+        << N[node + 1] << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
         << ", tmin, closest, tb, bn, bf, g, C);\n"
         << "      closest = sub ? tb : closest;\n      code = sub ? " << kBvhCode << "u : code;\n"
         << "      bhn = sub ? bn : bhn;\n      bhf = sub ? bf : bhf;\n    }\n";

@@ -780,6 +780,14 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
   return false;
 }
 
+// A BVH subtree [node, stop) walked per lane: its ordered BVH when it has one (obvh != 0),
+// otherwise (and always in the op-counting build) the reference tree in the reference order.
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
+__device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
+                            d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
+                            double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
+                            Rng& g, Ctr<COUNT>& C);
+
 template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB, bool VOLI>
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
@@ -929,9 +937,9 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
           const unsigned long long pt0 = __builtin_readcyclecounter();
           prof_steps[threadIdx.x] = 0u;
 #endif
-          const bool sub = traverse<MAIN, COUNT, VOLB, false, BVH>(P, node, h.y, wo, wd, tm, o, d,
-                                                                 frame, tmin, closest, t, hn, hf,
-                                                                 g, C);
+          const bool sub = bvh_subtree<MAIN, COUNT, VOLB, BVH>(P, node, h.y, h.w, wo, wd, tm, o,
+                                                             d, frame, tmin, closest, t, hn, hf,
+                                                             g, C);
 #ifdef RT_PROF
           {
             const unsigned long long dt = __builtin_readcyclecounter() - pt0;
@@ -996,6 +1004,147 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
   return hit;
 }
 
+
+// The ordered-BVH walk (rt_layout.h OBVH, rt_obvh.cpp) of one lane over the same leaf records as
+// the reference subtree. Every candidate is computed with the reference walker's arithmetic
+// (aquad_core / quad_test / sphere_test_v), but without the running upper bound: a quad's t
+// (inclusive [tmin, inf)), a sphere's near root in (tmin, inf) else its far root. The closest
+// candidate wins; away from ties that is the record the reference order returns. The lane is
+// flagged (the caller re-walks the reference tree in the reference order) when its result could
+// depend on the order: a candidate within kTieRel (relative) of the running closest t (which
+// starts at the caller's tmax), or a winner within kTieRel of tmin. Boxes are padded bounds and
+// the slab test keeps every box whose entry is <= closest * (1 + kTieRel), so no candidate the
+// flag logic must see is culled.
+constexpr double kTieRel = 0x1p-30;
+template <bool MAIN>
+__device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double tm, int frame,
+                          double tmin, double tmax, double& t_out, uint32_t& hit_node,
+                          int& hit_frame, bool& flag) {
+  const gptr N = (gptr)P.nodes;
+  const uint4 hd = ld4u(N + ob);  // n_entries, n_boxes, boxes_off, streams_off
+  const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+  const uint2* S = reinterpret_cast<const uint2*>(N + ob + hd.w) + (size_t)oct * hd.x;
+  const double* B = reinterpret_cast<const double*>(N + ob + hd.z);
+  const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
+  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
+  const double inv_a[3] = {inv.x, inv.y, inv.z}, oo[3] = {o.x, o.y, o.z};
+  double closest = tmax;
+  bool hit = false, tie = false;
+  uint32_t hn = 0;
+  uint32_t e = 0;
+  // one candidate: a tie test against the running closest, then the strict-min update
+  auto cand = [&](bool valid, double t, uint32_t rec) {
+    tie = tie | (valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel));
+    const bool win = valid & (t < closest);
+    closest = win ? t : closest;
+    hn = win ? rec : hn;
+    hit = hit | win;
+  };
+  for (;;) {
+    uint2 s = make_uint2(0u, 0u);
+    // while-while: box steps until a leaf (or the end), then the leaves with every lane that has
+    // one (as the reference-order LANE walker)
+    while (e < hd.x) {
+      s = S[e];
+      if (s.x & 0x80000000u) break;
+      const double* b = B + (size_t)s.y * 6;
+      const double2 bx = *reinterpret_cast<const double2*>(b);
+      const double2 by = *reinterpret_cast<const double2*>(b + 2);
+      const double2 bz = *reinterpret_cast<const double2*>(b + 4);
+      const double lo[3] = {bx.x, by.x, bz.x}, hi[3] = {bx.y, by.y, bz.y};
+      double tn = tmin, tf = closest * (1.0 + 2.0 * kTieRel);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double t0 = (lo[a] - oo[a]) * inv_a[a], t1 = (hi[a] - oo[a]) * inv_a[a];
+        const bool neg = inv_a[a] < 0.0;
+        tn = __builtin_fmax(tn, neg ? t1 : t0);  // a NaN slab bound leaves the interval alone
+        tf = __builtin_fmin(tf, neg ? t0 : t1);
+      }
+      e = (tn <= tf) ? e + 1u : s.x;
+    }
+    if (e >= hd.x) break;
+    const uint32_t rec = s.y;
+    const uint32_t ty = N[rec] & 0xffu;
+    if (ty == RTL_SPHERE) {
+      const gptr X = N + rec;
+      d3 c = ld3(X, 0);
+      if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
+      const double rad = ldd(X, 3);
+      const d3 oc = o - c;
+      const double a = dot(d, d);
+      const double half_b = dot(oc, d);
+      const double cc = dot(oc, oc) - rad * rad;
+      const double disc = fma(half_b, half_b, -(a * cc));
+      const bool real = !(disc < 0.0);
+      const double sqrtd = sqrt_nr(disc);
+      const double ra = rcp_nr(a);
+      const double nr = (-half_b - sqrtd) * ra;
+      const double fr = (sqrtd - half_b) * ra;
+      const bool in_n = (tmin < nr) & (nr < kInf), in_f = (tmin < fr) & (fr < kInf);
+      cand(real & (in_n | in_f), in_n ? nr : fr, rec);
+    } else {
+      const bool batch = ty == RTL_QUADS;
+      const uint32_t cnt = batch ? (N[rec] >> 8) : 1u;
+      gptr Q = batch ? N + rec + 4 : N + rec;
+      uint32_t qrec = batch ? rec + 4 : rec;
+      for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS, qrec += RTL_QUAD_WORDS) {
+        const AQuad q = load_aquad(Q);
+        const uint32_t axis = RTL_QUAD_AXIS(q.h0);
+        double t, a, b, dk;
+        if (axis == 1u) {
+          aquad_core<0>(q, o, d, r, t, a, b);
+          dk = d.x;
+        } else if (axis == 2u) {
+          aquad_core<1>(q, o, d, r, t, a, b);
+          dk = d.y;
+        } else if (axis == 3u) {
+          aquad_core<2>(q, o, d, r, t, a, b);
+          dk = d.z;
+        } else {  // quad_test's arithmetic (object.rs:453-490)
+          const gptr G = Q + RTL_QUAD_GEN;
+          const d3 n = ld3(G, 0);
+          dk = dot(n, d);
+          t = div_nr(ldd(G, 3) - dot(n, o), dk);
+          const d3 pq = vfma(t, d, o) - ld3(G, 4);
+          a = dot(pq, ld3(G, 8));
+          b = dot(pq, ld3(G, 12));
+        }
+        const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+        cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & !(lo < 0.0) & !(1.0 < hi), t, qrec);
+      }
+    }
+    ++e;
+  }
+  flag = tie | (hit & (closest <= tmin * (1.0 + kTieRel)));
+  if (hit) {
+    t_out = closest;
+    if (MAIN) {
+      hit_node = hn;
+      hit_frame = frame;
+    }
+  }
+  return hit;
+}
+
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
+__device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
+                            d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
+                            double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
+                            Rng& g, Ctr<COUNT>& C) {
+  if constexpr (!COUNT) {
+    if (obvh != 0u && !(P.flags & RT_FLAG_REFERENCE_BVH)) {
+      bool flag = false;
+      bool h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,
+                               flag);
+      if (__ballot(flag) != 0ull && flag)  // rare: the reference order decides
+        h = traverse<MAIN, COUNT, VOLB, false, BVH>(P, node, stop, wo, wd, tm, o, d, frame, tmin,
+                                                    tmax, t_out, hit_node, hit_frame, g, C);
+      return h;
+    }
+  }
+  return traverse<MAIN, COUNT, VOLB, false, BVH>(P, node, stop, wo, wd, tm, o, d, frame, tmin,
+                                                 tmax, t_out, hit_node, hit_frame, g, C);
+}
 
 // ---------------------------------------------------------------- textures
 __device__ __forceinline__ int32_t f2i_sat(double f) {  // Rust `as i32`

@@ -73,7 +73,15 @@
  *                                                                             object.rs:73-105 */
 #define RTL_SPHERE_MOVING 0x100u
 #define RTL_SPHERE_WORDS 20
-/* BVH (16 words): [hdr][skip][child][0] d0-5 xmin xmax ymin ymax zmin zmax  hittable.rs:135-187 */
+/* BVH (16 words): [hdr][skip][child][obvh] d0-5 xmin xmax ymin ymax zmin zmax hittable.rs:135-187
+ *   obvh: word offset of the subtree's ordered BVH (below), 0 = none (walk the reference tree).
+ * OBVH (rt_obvh.cpp), for a BVH subtree whose leaves are QUAD / QUADS / SPHERE records: an SAH
+ * BVH2 over the same leaf records, appended after the record region (n_rec_words):
+ *   [n_entries][n_boxes][boxes_off][streams_off]      (offsets in words from the OBVH header)
+ *   boxes: n_boxes x 12 words, f64 xmin xmax ymin ymax zmin zmax (conservative: padded bounds)
+ *   streams: 8 ray-direction octants (bit a set = d_a < 0) x n_entries x 2 words, each a
+ *   threaded pre-order walk with the near child first: internal [skip][box] (box hit -> next
+ *   entry, miss -> skip), leaf [0x80000000][record] (then the next entry). */
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
@@ -126,4 +134,5 @@ typedef struct rtl_scene_header {
   uint32_t volume_in_bvh; /* a ConstantMedium lies inside a BVH subtree                */
   uint32_t volumes_one_walk_spheres; /* every ConstantMedium boundary is a one-walk sphere */
   uint32_t has_isotropic; /* some material is Isotropic (also outside a ConstantMedium)  */
+  uint32_t n_rec_words;   /* node words holding records; ordered BVHs follow (OBVH below) */
 } rtl_scene_header;

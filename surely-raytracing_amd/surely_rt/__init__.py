@@ -35,6 +35,7 @@ RT_FLAG_OVERWRITE = 0x1
 RT_FLAG_COUNT_OPS = 0x2
 RT_FLAG_SEMANTICS_REFERENCE = 0x4
 RT_FLAG_INTERPRETER = 0x8  # product render with the interpreter walker (no scene-specialised kernel)
+RT_FLAG_REFERENCE_BVH = 0x10  # product render walks BVH subtrees in the reference tree and order
 
 OP_NAMES = [
     "samples", "world_queries", "quad_tests", "quad_plane", "quad_interval", "quad_hits",
@@ -484,7 +485,7 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
 
 
 LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
-                "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights"]
+                "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs"]
 
 
 def layout_stats(blob: "Blob") -> dict:

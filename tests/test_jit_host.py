@@ -20,7 +20,7 @@ def test_generated_walker_compiles(name):
     assert state == 1, msg
     assert "struct TravGen" in msg
     # a BVH subtree record hands its [root, skip) range to the per-lane walker
-    n_calls = len(re.findall(r"traverse<true, COUNT, VOLB, false, BVH>", msg))
+    n_calls = len(re.findall(r"bvh_subtree<true, COUNT, VOLB, BVH>", msg))
     assert (n_calls > 0) == (rt.layout_stats(blob)["bvh_records"] > 0)
 
 
@@ -30,13 +30,14 @@ def test_final_scene_walker_bvh_calls():
     blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
     state, src = rt.jit_check(blob)
     assert state == 1, src
-    calls = re.findall(r"traverse<true, COUNT, VOLB, false, BVH>\(P, (\d+)u, (\d+)u, ro, rd, tm, o, d, "
-                       r"(-?\d+),", src)
+    calls = re.findall(r"bvh_subtree<true, COUNT, VOLB, BVH>\(P, (\d+)u, (\d+)u, (\d+)u, ro, rd, tm, "
+                       r"o, d, (-?\d+),", src)
     assert len(calls) == 2
-    assert calls[0][2] == "-1" and calls[1][2] != "-1"
-    # the subtree's skip is the record the generated walk continues with
-    for root, skip, _ in calls:
-        assert int(skip) > int(root)
+    assert calls[0][3] == "-1" and calls[1][3] != "-1"
+    # the subtree's skip is the record the generated walk continues with; both subtrees (boxes,
+    # spheres) have an ordered BVH (rt_obvh.cpp), appended after the records
+    for root, skip, obvh, _ in calls:
+        assert int(skip) > int(root) and int(obvh) > int(skip)
     assert src.index("translate_in") < src.index("rotate_y_in") < src.index(f"P, {calls[1][0]}u")
 
 

@@ -57,3 +57,17 @@ def test_span1_duplicates_are_marked():
     st = rt.layout_stats(blob)
     # 5 objects: span 5 -> (2, 3); 3 -> (1, 2): five BvhNodes, one of span 1
     assert st["bvh_records"] == 5 and st["dup_records"] == 1
+
+
+def test_ordered_bvhs_for_primitive_leaf_subtrees():
+    """rt_obvh.cpp: final_scene's two BVH subtrees (400 ground boxes = quad batches; 1000 spheres
+    under Translate(RotateY)) get ordered BVHs; a BVH whose leaves hold instances does not."""
+    blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
+    assert rt.layout_stats(blob)["ordered_bvhs"] == 2
+    sc = rt.Scene(21)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    items = sc.hittable_list(sc.translate(sc.make_box((0, 0, 0), (1, 1, 1), white), (2, 0, 0)),
+                             sc.sphere((0, 0, 0), 0.5, white), sc.sphere((0, 2, 0), 0.5, white))
+    world = sc.hittable_list(sc.create_bvh(items))
+    st = rt.layout_stats(sc.serialize(world, None))
+    assert st["bvh_records"] > 0 and st["ordered_bvhs"] == 0

@@ -40,9 +40,11 @@ for r in range(ROUNDS + 1):
     for p, lib, h in zip(paths, libs, scenes):
         acc = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
         st = rt.RtStats()
-        saved = {k: os.environ.get(k) for k in envs[p]}
-        os.environ.update(envs[p])
-        assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
+        ev = dict(envs[p])
+        o2 = rt.make_opts(cam, seed=1, flags=rt.RT_FLAG_OVERWRITE | int(ev.pop("FLAGS", "0"), 0))
+        saved = {k: os.environ.get(k) for k in ev}
+        os.environ.update(ev)
+        assert lib.rt_render(h, C.byref(cam), C.byref(o2), acc.ctypes.data, C.byref(st)) == 0
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k)
