@@ -243,6 +243,10 @@ int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts
 #define RT_TRACE_HISTORY 64
 int rt_scene_trace_ms(rt_scene* scene, float* ms_out, int max_n, int* n_out);
 
+/* Diagnostics: counters of a profiling build of the library (-DRT_PROF, tools_gpu/); zeros in
+ * the product build. */
+int rt_scene_prof_counters(rt_scene* scene, uint64_t* out, int n);
+
 /* One-shot drop-in for render_par_lights: create + render + destroy. */
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
                    float* accum_rgb, rt_stats* stats);

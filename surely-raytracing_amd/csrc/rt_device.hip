@@ -388,6 +388,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.root = sc->hdr.root;
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
+  P.lights_nested = sc->hdr.lights_nested;
   P.inv_n_lights = sc->hdr.n_lights ? 1.0 / (double)sc->hdr.n_lights : 0.0;
   P.sphere_light0 = sc->sphere_light0;
   P.flags = opts->flags;
@@ -595,6 +596,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   double* tot = (double*)sc->work;
   P.part = (double*)(sc->work + tot_bytes);
   if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
+#ifdef RT_PROF
+  HIP_TRY(hipMemsetAsync(sc->ops + 40, 0, sizeof(unsigned long long) * 21, stream));
+#endif
   if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
   uint64_t out_bytes = 0;
   uint32_t launches = 0;
@@ -648,6 +652,20 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     stats->ms_total =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  return RT_OK;
+}
+
+// Profiling builds (-DRT_PROF, not shipped): the ordered-BVH walk counters of the last render
+// (rt_kernel.h obvh_walk). Other builds return zeros.
+int rt_scene_prof_counters(rt_scene* sc, uint64_t* out, int n) {
+  if (!sc || !out || n < 0) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lock(sc->mu);
+  HIP_TRY(hipSetDevice(sc->device));
+  unsigned long long h[24] = {};
+#ifdef RT_PROF
+  HIP_TRY(hipMemcpy(h, sc->ops + 40, sizeof(h), hipMemcpyDeviceToHost));
+#endif
+  for (int k = 0; k < n && k < 24; ++k) out[k] = h[k];
   return RT_OK;
 }
 

@@ -153,6 +153,8 @@ struct Emitter {
 
   // conservative bounds of the leaf records emitted (pre-relocation position), for rt_obvh.cpp
   std::vector<std::pair<size_t, PrimBox>> pbox;
+  // transform chains longer than RTL_MAX_CHAIN (pre-relocation positions, root first)
+  std::vector<std::vector<uint32_t>> long_chains;
 
   explicit Emitter(std::vector<uint32_t>& words, int64_t nm) : w(words), n_mats(nm) {}
 
@@ -371,16 +373,18 @@ struct Emitter {
       case RT_OBJ_SPHERE: sphere(n, false); break;
       case RT_OBJ_TRANSLATE:
       case RT_OBJ_ROTATE_Y: {
-        if (chain.size() >= RTL_MAX_CHAIN) {
-          fail(RT_ERR_UNSUPPORTED, "more than 4 nested Translate/RotateY instances");
-          return;
-        }
         bool tr = n.tag == RT_OBJ_TRANSLATE;
         size_t p = push(tr ? RTL_TRANSLATE : RTL_ROTATE_Y, RTL_XFORM_WORDS);
         chain.push_back((uint32_t)p);
         if (chain.size() > max_chain) max_chain = (uint32_t)chain.size();
         w[p + 2] = (uint32_t)chain.size();
-        for (size_t k = 0; k < chain.size(); ++k) w[p + 4 + k] = chain[k];
+        if (chain.size() <= RTL_MAX_CHAIN) {
+          for (size_t k = 0; k < chain.size(); ++k) w[p + 4 + k] = chain[k];
+        } else {  // a long chain: table appended after relocation (flatten)
+          w[p] |= RTL_XFORM_LONG;
+          w[p + 4] = (uint32_t)long_chains.size();
+          long_chains.push_back(chain);
+        }
         if (tr) {
           putd(w, p, 2, n.f[0]), putd(w, p, 3, n.f[1]), putd(w, p, 4, n.f[2]);
         } else {
@@ -470,7 +474,7 @@ void relocate(std::vector<uint32_t>& w, uint32_t* root, uint32_t* bvh_words,
     } else if (type != RTL_END) {
       out[q + 3] = m((uint32_t)(p + sz));  // pre-order successor
     }
-    if (type == RTL_TRANSLATE || type == RTL_ROTATE_Y)
+    if ((type == RTL_TRANSLATE || type == RTL_ROTATE_Y) && !(h & RTL_XFORM_LONG))
       for (uint32_t k = 0; k < w[p + 2]; ++k) out[q + 4 + k] = m(w[p + 4 + k]);  // chain
     if (type == RTL_EXIT) out[q + 2] = m(w[p + 2]);  // parent frame
   }
@@ -683,6 +687,16 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   std::vector<uint32_t> map;
   relocate(F.nodes, &root, &bvh_words, &map);
   const uint32_t rec_words = (uint32_t)F.nodes.size();
+  // long transform chains (rt_layout.h RTL_XFORM_LONG): relocated tables after the records
+  for (size_t p = 0; p < rec_words; p += record_words(F.nodes[p])) {
+    const uint32_t h = F.nodes[p], ty = h & 0xffu;
+    if ((ty == RTL_TRANSLATE || ty == RTL_ROTATE_Y) && (h & RTL_XFORM_LONG)) {
+      const std::vector<uint32_t>& c = em.long_chains[F.nodes[p + 4]];
+      F.nodes[p + 4] = (uint32_t)F.nodes.size();
+      for (uint32_t x : c) F.nodes.push_back(map[x]);
+    }
+  }
+  while (F.nodes.size() % 4) F.nodes.push_back(0u);
   {  // ordered BVHs of the product kernels (rt_obvh.cpp), appended after the records
     std::vector<PrimBox> boxes(rec_words);
     for (auto& pb : em.pbox)
@@ -694,7 +708,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
     return RT_ERR_UNSUPPORTED;
   }
   // lights (HittablePDF over the lights object, pdf.rs:80-100)
-  uint32_t n_lights = 0, is_list = 0;
+  uint32_t n_lights = 0, is_list = 0, lights_nested = 0;
   if (lights_off >= 0) {
     Reader lr{s, n, (uint64_t)lights_off};
     auto lights = lr.err ? nullptr : read_node(lr, 0);
@@ -703,25 +717,55 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
       return RT_ERR_BAD_BLOB;
     }
     Emitter le(F.lights, (int64_t)n_mat);
-    auto one = [&](const Node& nd) {
-      F.light_offs.push_back((uint32_t)F.lights.size());
-      if (nd.tag == RT_OBJ_QUAD) le.quad(nd, true);
-      else if (nd.tag == RT_OBJ_SPHERE) le.sphere(nd, true);
-      else le.push(RTL_OTHER, 4);
-    };
+    // Light entries: the top-level objects first, then the children of every nested list
+    // (object.rs:57, 66: Object::List dispatches pdf_value / random to HittableList) as one
+    // consecutive block per list, breadth first.
+    std::vector<const Node*> ent;
+    std::vector<int> level;
+    std::vector<uint32_t> first;
     if (lights->tag == RT_OBJ_LIST) {
       is_list = 1;
-      for (auto& k : lights->kids) {
-        if (k->tag == RT_OBJ_LIST) {
-          *err = "nested HittableList inside the light list";
-          return RT_ERR_UNSUPPORTED;
-        }
-        one(*k);
-      }
+      for (auto& k : lights->kids) ent.push_back(k.get()), level.push_back(1);
     } else {
-      one(*lights);
+      ent.push_back(lights.get()), level.push_back(1);
     }
-    n_lights = (uint32_t)F.light_offs.size();
+    n_lights = (uint32_t)ent.size();
+    first.assign(ent.size(), 0u);
+    for (size_t e = 0; e < ent.size(); ++e) {
+      if (ent[e]->tag != RT_OBJ_LIST || (e == 0 && !is_list && ent[e] == lights.get())) continue;
+      if (ent[e]->kids.empty()) {
+        *err = "empty HittableList inside the light list: the reference panics (hittable.rs:120)";
+        return RT_ERR_EMPTY_LIGHTS;
+      }
+      if (level[e] > RTL_LIGHT_NEST) {
+        *err = "light lists nested deeper than " + std::to_string(RTL_LIGHT_NEST);
+        return RT_ERR_UNSUPPORTED;
+      }
+      first[e] = (uint32_t)ent.size();
+      for (auto& k : ent[e]->kids) {
+        ent.push_back(k.get()), level.push_back(level[e] + 1), first.push_back(0u);
+      }
+    }
+    for (size_t e = 0; e < ent.size(); ++e) {
+      const Node& nd = *ent[e];
+      F.light_offs.push_back((uint32_t)F.lights.size());
+      if (nd.tag == RT_OBJ_QUAD) {
+        le.quad(nd, true);
+      } else if (nd.tag == RT_OBJ_SPHERE) {
+        le.sphere(nd, true);
+      } else if (nd.tag == RT_OBJ_LIST && e < F.light_offs.size() && first[e] != 0u) {
+        const size_t p = le.push(RTL_LLIST | (uint32_t)(nd.kids.size() << 8), RTL_LLIST_WORDS);
+        F.lights[p + 1] = first[e];
+        putd(F.lights, p, 0, 1. / (double)nd.kids.size());  // hittable.rs:116
+        lights_nested = 1;
+      } else {
+        le.push(RTL_OTHER, 4);
+      }
+    }
+    if (le.status != RT_OK) {
+      *err = le.err;
+      return le.status;
+    }
     if (is_list && n_lights == 0) {
       // An empty HittableList light object panics in the reference exactly like render_par.
       is_list = 0;
@@ -738,6 +782,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.n_perlins = (uint32_t)n_perl;
   h.n_lights = n_lights;
   h.lights_is_list = is_list;
+  h.lights_nested = lights_nested;
   h.has_bvh = em.has_bvh;
   h.has_volume = em.has_volume;
   h.volume_in_bvh = em.volume_in_bvh;

@@ -23,6 +23,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -55,6 +56,10 @@ double word_double(const std::vector<uint32_t>& N, size_t w) {
 double pd(const std::vector<uint32_t>& N, size_t rec, int k) { return word_double(N, rec + 4 + 2 * k); }
 
 std::string lit(double v) {  // exact: hex-float literal of the same bits
+  // (%a prints non-finite values as inf / nan, which are not C++ literals: a degenerate quad's
+  // normal, unit(0) = NaN, is valid reference input)
+  if (std::isnan(v)) return "(__builtin_nan(\"\"))";
+  if (std::isinf(v)) return v > 0 ? "(__builtin_inf())" : "(-__builtin_inf())";
   char b[64];
   std::snprintf(b, sizeof b, "(%a)", v);
   return b;
@@ -135,7 +140,7 @@ bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostri
   std::ostringstream b;
   size_t x = N[node + 3];
   for (int guard = 0;; ++guard) {  // the instance chain in front of the primitive(s)
-    if (x + 4 > N.size() || guard > RTL_MAX_CHAIN + 8) return false;
+    if (x + 4 > N.size() || guard > 4096) return false;
     const uint32_t ty = N[x] & 0xffu;
     if (ty == RTL_TRANSLATE) {
       b << "    translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4)) << ", o);\n";
@@ -217,6 +222,81 @@ bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostri
 // The light-list PDF value of the mixture (rt_kernel.h light_pdf: HittableList::pdf_value
 // hittable.rs:115-124 over Quad/Sphere::pdf_value object.rs:492-501, 190-202), the list unrolled
 // with each light's constants as literals: the same expressions in the same order.
+// Straight-line code for light entry i (rt_kernel.h light_entry_pdf): sets `pv`.
+bool gen_light_entry(const rtf::FlatScene& F, size_t i, int nest, int sphere0, int& uid,
+                     std::ostringstream& o, std::string* why) {
+  const std::vector<uint32_t>& L = F.lights;
+  if (i >= F.light_offs.size() || F.light_offs[i] + 4 > L.size()) {
+    *why = "malformed light table";
+    return false;
+  }
+  const size_t off = F.light_offs[i];
+  const uint32_t type = L[off] & 0xffu;
+  o << "    // light " << i << "\n    pv = 0.0;\n";
+  if (type == RTL_LLIST) {  // a nested HittableList: left fold of its children, times 1/len
+    if (nest <= 0) {
+      *why = "light lists nested too deep";
+      return false;
+    }
+    const uint32_t n = L[off] >> 8, first = L[off + 1];
+    const std::string acc = "lsum" + std::to_string(uid++);
+    o << "    {\n    double " << acc << " = 0.0;\n";
+    for (uint32_t k = 0; k < n; ++k) {
+      if (!gen_light_entry(F, first + k, nest - 1, sphere0, uid, o, why)) return false;
+      o << "    " << acc << (k == 0 ? " = pv;\n" : " = " + acc + " + pv;\n");
+    }
+    o << "    pv = " << acc << " * " << lit(pd(L, off, 0)) << ";\n    }\n";
+  } else if (type == RTL_QUAD) {
+    o << "    {\n      C.inc(RT_OP_LIGHT_PDF_QUAD);\n      double t = 0.0;\n      bool hq;\n";
+    const uint32_t axis = RTL_QUAD_AXIS(L[off]);
+    if (axis) {
+      const int k = (int)axis - 1;
+      const char* r[3] = {"0.", "0.", "0."};
+      const char* rc[3] = {"rcp_nr1(dir.x)", "rcp_nr1(dir.y)", "rcp_nr1(dir.z)"};
+      r[k] = rc[k];
+      o << "      hq = aquad_test<COUNT, " << k << ">(AQuad{" << L[off] << "u";
+      for (int j = 0; j < 5; ++j) o << ", " << lit(pd(L, off, RTL_LQUAD_AXIS_D + j));
+      o << "}, origin, dir, mk(" << r[0] << ", " << r[1] << ", " << r[2]
+        << "), 0.001, kInf, t, C);\n";
+    } else {
+      o << "      hq = quad_test<COUNT>((kptr)P.lights + " << off
+        << "u, origin, dir, 0.001, kInf, t, C);\n";
+    }
+    o << "      const double len2 = dot(dir, dir);\n"
+         "      const double dist2 = (t * t) * len2;\n"
+         "      const double cosine = fabs(dot(dir, "
+      << lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2))
+      << ")) * rsq_nr(len2);\n"
+         "      const double q = dist2 * rcp_w(cosine * "
+      << lit(pd(L, off, 7)) << ");\n      pv = hq ? q : 0.0;\n    }\n";
+  } else if (type == RTL_SPHERE) {
+    const std::string c = lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2));
+    const std::string r = lit(pd(L, off, 3));
+    o << "    {\n      C.inc(RT_OP_LIGHT_PDF_SPHERE);\n      bool hs;\n"
+         "      if (COUNT) {\n        double t = 0.0;\n"
+         "        hs = sphere_test<COUNT>((kptr)P.lights + " << off
+      << "u, origin, dir, 0.0, 0.001, kInf, t, C);\n      } else {\n"
+         "        const d3 oc = origin - " << c << ";\n"
+         "        const double a = dot(dir, dir);\n"
+         "        const double half_b = dot(oc, dir);\n"
+         "        const double r = " << r << ";\n"
+         "        const double c = dot(oc, oc) - r * r;\n"
+         "        const double disc = fma(half_b, half_b, -(a * c));\n"
+         "        const double c1 = fma(0.001, a, half_b);\n"
+         "        hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));\n      }\n"
+         "      double cos_max = 0.0;\n";
+    if ((int)i == sphere0) {
+      o << "      cos_max = cos_sl0;\n";
+    } else {
+      o << "      if (hs) {\n        d3 cmo = " << c << " - origin;\n        double r = " << r
+        << ";\n        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));\n      }\n";
+    }
+    o << "      const double solid = 2.0 * kPi * (1.0 - cos_max);\n"
+         "      const double q = rcp_w(solid);\n      pv = hs ? q : 0.0;\n    }\n";
+  }
+  return true;
+}
+
 bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string* why) {
   const std::vector<uint32_t>& L = F.lights;
   o << "  template <bool COUNT>\n"
@@ -230,67 +310,14 @@ bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string*
       sphere0 = (int)i;
       break;
     }
-  const size_t n = F.hdr.n_lights;  // the interpreter's P.n_lights
+  const size_t n = F.hdr.n_lights;  // the interpreter's P.n_lights (top-level entries)
   if (n > F.light_offs.size()) {
     *why = "malformed light table";
     return false;
   }
+  int uid = 0;
   for (size_t i = 0; i < n; ++i) {
-    const size_t off = F.light_offs[i];
-    if (off + 4 > L.size()) {
-      *why = "malformed light table";
-      return false;
-    }
-    const uint32_t type = L[off] & 0xffu;
-    o << "    // light " << i << "\n    pv = 0.0;\n";
-    if (type == RTL_QUAD) {
-      o << "    {\n      C.inc(RT_OP_LIGHT_PDF_QUAD);\n      double t = 0.0;\n      bool hq;\n";
-      const uint32_t axis = RTL_QUAD_AXIS(L[off]);
-      if (axis) {
-        const int k = (int)axis - 1;
-        const char* r[3] = {"0.", "0.", "0."};
-        const char* rc[3] = {"rcp_nr1(dir.x)", "rcp_nr1(dir.y)", "rcp_nr1(dir.z)"};
-        r[k] = rc[k];
-        o << "      hq = aquad_test<COUNT, " << k << ">(AQuad{" << L[off] << "u";
-        for (int j = 0; j < 5; ++j) o << ", " << lit(pd(L, off, RTL_LQUAD_AXIS_D + j));
-        o << "}, origin, dir, mk(" << r[0] << ", " << r[1] << ", " << r[2]
-          << "), 0.001, kInf, t, C);\n";
-      } else {
-        o << "      hq = quad_test<COUNT>((kptr)P.lights + " << off
-          << "u, origin, dir, 0.001, kInf, t, C);\n";
-      }
-      o << "      const double len2 = dot(dir, dir);\n"
-           "      const double dist2 = (t * t) * len2;\n"
-           "      const double cosine = fabs(dot(dir, "
-        << lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2))
-        << ")) * rsq_nr(len2);\n"
-           "      const double q = dist2 * rcp_w(cosine * "
-        << lit(pd(L, off, 7)) << ");\n      pv = hq ? q : 0.0;\n    }\n";
-    } else if (type == RTL_SPHERE) {
-      const std::string c = lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2));
-      const std::string r = lit(pd(L, off, 3));
-      o << "    {\n      C.inc(RT_OP_LIGHT_PDF_SPHERE);\n      bool hs;\n"
-           "      if (COUNT) {\n        double t = 0.0;\n"
-           "        hs = sphere_test<COUNT>((kptr)P.lights + " << off
-        << "u, origin, dir, 0.0, 0.001, kInf, t, C);\n      } else {\n"
-           "        const d3 oc = origin - " << c << ";\n"
-           "        const double a = dot(dir, dir);\n"
-           "        const double half_b = dot(oc, dir);\n"
-           "        const double r = " << r << ";\n"
-           "        const double c = dot(oc, oc) - r * r;\n"
-           "        const double disc = fma(half_b, half_b, -(a * c));\n"
-           "        const double c1 = fma(0.001, a, half_b);\n"
-           "        hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));\n      }\n"
-           "      double cos_max = 0.0;\n";
-      if ((int)i == sphere0) {
-        o << "      cos_max = cos_sl0;\n";
-      } else {
-        o << "      if (hs) {\n        d3 cmo = " << c << " - origin;\n        double r = " << r
-          << ";\n        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));\n      }\n";
-      }
-      o << "      const double solid = 2.0 * kPi * (1.0 - cos_max);\n"
-           "      const double q = rcp_w(solid);\n      pv = hs ? q : 0.0;\n    }\n";
-    }
+    if (!gen_light_entry(F, i, RTL_LIGHT_NEST, sphere0, uid, o, why)) return false;
     o << (i == 0 ? "    sum = pv;\n" : "    sum = sum + pv;\n");
   }
   if (F.hdr.lights_is_list && n) {
@@ -356,7 +383,9 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
       G.frame_changed();
       if (frame >= 0) {
         const uint32_t len = N[(size_t)frame + 2];
-        for (uint32_t k = 0; k < len && k < RTL_MAX_CHAIN; ++k) G.xform(N[(size_t)frame + 4 + k]);
+        const bool lng = (N[(size_t)frame] & RTL_XFORM_LONG) != 0u;
+        for (uint32_t k = 0; k < len; ++k)
+          G.xform(lng ? N[(size_t)N[(size_t)frame + 4] + k] : N[(size_t)frame + 4 + k]);
       }
       node = N[node + 3];
     } else if (ty == RTL_VOLUME) {
@@ -512,6 +541,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #endif
 #ifdef RT_ABL_HIT2
   opts.push_back("-DRT_ABL_HIT2");
+#endif
+#ifdef RT_ABL_TWICE_BVH
+  opts.push_back("-DRT_ABL_TWICE_BVH=" RTJ_STR(RT_ABL_TWICE_BVH));
 #endif
 #ifdef RT_ABL_NOXS
   opts.push_back("-DRT_ABL_NOXS");

@@ -232,6 +232,7 @@ struct TraceParams {
   int n_pairs_a;  // (tile, s_j) pairs rendered as whole stratum rows per lane
   int n_blk;      // s_i blocks per tail pair: ceil(sqrt_spp / kPoolSi)
   uint32_t root, n_lights, lights_is_list, flags;
+  uint32_t lights_nested;  // some light entry is a nested HittableList (RTL_LLIST)
   int sphere_light0;    // index of the first SPHERE light record, -1 if none
   double inv_n_lights;  // 1.0 / n_lights (host IEEE division, hittable.rs:116)
   uint32_t n_perlin_lds;  // Perlin tables readable from LDS (TEX kernels)
@@ -567,6 +568,10 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
   if (frame < 0) return;
   uint4 h = ld4u(N + frame);
   uint4 ch = ld4u(N + frame + 4);
+  if (h.x & RTL_XFORM_LONG) {  // chain in the appended table (rt_layout.h)
+    for (uint32_t k = 0; k < h.z; ++k) xform_in(N + N[ch.x + k], o, d);
+    return;
+  }
   const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
 #pragma unroll
   for (int k = 0; k < RTL_MAX_CHAIN; ++k)
@@ -1021,49 +1026,66 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
                           int& hit_frame, bool& flag) {
   const gptr N = (gptr)P.nodes;
-  const uint4 hd = ld4u(N + ob);  // n_entries, n_boxes, boxes_off, streams_off
-  const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
-  const uint2* S = reinterpret_cast<const uint2*>(N + ob + hd.w) + (size_t)oct * hd.x;
-  const double* B = reinterpret_cast<const double*>(N + ob + hd.z);
+  const uint4 hd = ld4u(N + ob);  // n_entries, 0, 0, streams_off
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
+  // octant by sign bit (1/-0 = -inf: the near bound of that axis is its max)
+  const uint32_t oct = (inv.x < 0.0 ? 1u : 0u) | (inv.y < 0.0 ? 2u : 0u) | (inv.z < 0.0 ? 4u : 0u);
+  const uint4* S = reinterpret_cast<const uint4*>(N + ob + hd.w) + (size_t)oct * hd.x * 2;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
-  const double inv_a[3] = {inv.x, inv.y, inv.z}, oo[3] = {o.x, o.y, o.z};
+  // Box steps in f32 (the bounds were rounded outwards with a 2^-18 (1 + |coord|) margin,
+  // rt_obvh.cpp). Error budget of a slab time t_a = (bound - o_a) * inv_a: the f32 roundings
+  // of o (2^-24 |o_a| <= 2^-24 (|bound| + |bound - o_a|): the first part is inside the margin,
+  // the second is relative to t_a), of inv, of the difference and of the product: a few 2^-24
+  // relative, so the interval is widened by kBoxRel = 2^-20 on both ends. Culling therefore
+  // never drops a box holding a candidate <= closest * (1 + kTieRel).
+  constexpr float kBoxRel = 0x1p-20f;
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
+  const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
   double closest = tmax;
-  bool hit = false, tie = false;
+  float close_f = (float)(closest + closest * (2.0 * kTieRel));
+  bool hit = false;
+  double tie_at = -1.0;  // running closest at the latest near-tie (the winner's t or earlier)
   uint32_t hn = 0;
   uint32_t e = 0;
-  // one candidate: a tie test against the running closest, then the strict-min update
+#ifdef RT_PROF  // profiling build: per-lane box steps / leaves, wave maxima, wave cycles
+  uint32_t pf_box = 0, pf_leaf = 0;
+  const unsigned long long pf_t0 = __builtin_readcyclecounter();
+#endif
+  // one candidate: a near-tie test against the running closest, then the strict-min update.
+  // Interior faces of touching boxes tie with each other before the ordered walk reaches the
+  // nearest hit; only a near-tie AT the final closest t can change the reference's record.
   auto cand = [&](bool valid, double t, uint32_t rec) {
-    tie = tie | (valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel));
+    const bool nt = valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel);
+    tie_at = nt ? closest : tie_at;
     const bool win = valid & (t < closest);
     closest = win ? t : closest;
     hn = win ? rec : hn;
     hit = hit | win;
   };
   for (;;) {
-    uint2 s = make_uint2(0u, 0u);
+    uint4 s = make_uint4(0u, 0u, 0u, 0u);
     // while-while: box steps until a leaf (or the end), then the leaves with every lane that has
     // one (as the reference-order LANE walker)
     while (e < hd.x) {
-      s = S[e];
+      s = S[2 * e];
       if (s.x & 0x80000000u) break;
-      const double* b = B + (size_t)s.y * 6;
-      const double2 bx = *reinterpret_cast<const double2*>(b);
-      const double2 by = *reinterpret_cast<const double2*>(b + 2);
-      const double2 bz = *reinterpret_cast<const double2*>(b + 4);
-      const double lo[3] = {bx.x, by.x, bz.x}, hi[3] = {bx.y, by.y, bz.y};
-      double tn = tmin, tf = closest * (1.0 + 2.0 * kTieRel);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const double t0 = (lo[a] - oo[a]) * inv_a[a], t1 = (hi[a] - oo[a]) * inv_a[a];
-        const bool neg = inv_a[a] < 0.0;
-        tn = __builtin_fmax(tn, neg ? t1 : t0);  // a NaN slab bound leaves the interval alone
-        tf = __builtin_fmin(tf, neg ? t0 : t1);
-      }
-      e = (tn <= tf) ? e + 1u : s.x;
+      const uint4 s2 = S[2 * e + 1];
+      const float tnx = (__uint_as_float(s.z) - ox) * ix, tfx = (__uint_as_float(s.w) - ox) * ix;
+      const float tny = (__uint_as_float(s2.x) - oy) * iy, tfy = (__uint_as_float(s2.y) - oy) * iy;
+      const float tnz = (__uint_as_float(s2.z) - oz) * iz, tfz = (__uint_as_float(s2.w) - oz) * iz;
+      // fmaxf / fminf drop a NaN bound (o on the bound's plane with inv = +-inf): no constraint
+      const float tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
+      const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
+      const bool pass = fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
+      e = pass ? e + 1u : s.x;
+#ifdef RT_PROF
+      ++pf_box;
+#endif
     }
     if (e >= hd.x) break;
     const uint32_t rec = s.y;
+    const double closest_before = closest;
     const uint32_t ty = N[rec] & 0xffu;
     if (ty == RTL_SPHERE) {
       const gptr X = N + rec;
@@ -1113,9 +1135,37 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
         cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & !(lo < 0.0) & !(1.0 < hi), t, qrec);
       }
     }
+    if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
     ++e;
+#ifdef RT_PROF
+    ++pf_leaf;
+#endif
   }
-  flag = tie | (hit & (closest <= tmin * (1.0 + kTieRel)));
+  flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
+         (hit & (closest <= tmin * (1.0 + kTieRel)));
+#ifdef RT_PROF
+  {
+    const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
+    uint32_t mb = pf_box, ml = pf_leaf;
+    for (int k = 32; k > 0; k >>= 1) {
+      mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
+      ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
+    }
+    // P.ops[40 + ...] (past the pool-queue word; rt_scene_prof_counters): per walk kind
+    // (0: world frame, 1: instance frame) 6 counters
+    unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
+    const unsigned long long fl = __popcll(__ballot(flag));
+    atomicAdd(&pc[0], (unsigned long long)pf_box);
+    atomicAdd(&pc[2], (unsigned long long)pf_leaf);
+    if (prof_first_lane()) {
+      atomicAdd(&pc[1], (unsigned long long)mb);
+      atomicAdd(&pc[3], (unsigned long long)ml);
+      atomicAdd(&pc[4], 1ull);
+      atomicAdd(&pc[5], dt);
+      atomicAdd(&P.ops[52], fl);  // lanes flagged for the reference-order re-walk
+    }
+  }
+#endif
   if (hit) {
     t_out = closest;
     if (MAIN) {
@@ -1131,6 +1181,19 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
                             Rng& g, Ctr<COUNT>& C) {
+#ifdef RT_ABL_TWICE_BVH  // ablation build: the top-level (1) / in-instance (2) ordered-BVH walk
+                         // runs twice (same image); the time delta is one walk's cost
+  if (!COUNT && obvh != 0u &&
+      ((RT_ABL_TWICE_BVH == 1 && frame < 0) || (RT_ABL_TWICE_BVH == 2 && frame >= 0))) {
+    double t2 = 0.0, z = 0.0;
+    uint32_t hn2 = 0;
+    int hf2 = -1;
+    bool f2 = false;
+    asm volatile("" : "+v"(z));
+    const bool h2 = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2);
+    asm volatile("" ::"v"(t2), "v"(hn2), "v"(h2), "v"(f2));
+  }
+#endif
   if constexpr (!COUNT) {
     if (obvh != 0u && !(P.flags & RT_FLAG_REFERENCE_BVH)) {
       bool flag = false;
@@ -1291,70 +1354,98 @@ __device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 
 // cos_sl0: cos_theta_max of the first sphere light at `origin` (object.rs:196), computed once per
 // bounce by the caller and shared with Sphere::random (the same expression, the same bits).
 template <bool COUNT>
+__device__ double light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
+                                 double cos_sl0, Ctr<COUNT>& C) {
+  const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
+  uint32_t type = L[0] & 0xffu;
+  double pv = 0.0;
+  if (type == RTL_QUAD) {
+    C.inc(RT_OP_LIGHT_PDF_QUAD);
+    double t = 0.0;
+    bool hq;
+    const uint32_t axis = RTL_QUAD_AXIS(L[0]);
+    if (axis) {  // axis-aligned form at d24 (rt_layout.h): the world quads' bit-identical test
+      const kdptr A = reinterpret_cast<kdptr>(L + 4) + RTL_LQUAD_AXIS_D;
+      const AQuad q = {L[0], A[0], A[1], A[2], A[3], A[4]};
+      if (axis == 1u) {
+        hq = aquad_test<COUNT, 0>(q, origin, dir, mk(rcp_nr1(dir.x), 0., 0.), 0.001, kInf, t, C);
+      } else if (axis == 2u) {
+        hq = aquad_test<COUNT, 1>(q, origin, dir, mk(0., rcp_nr1(dir.y), 0.), 0.001, kInf, t, C);
+      } else {
+        hq = aquad_test<COUNT, 2>(q, origin, dir, mk(0., 0., rcp_nr1(dir.z)), 0.001, kInf, t, C);
+      }
+    } else {
+      hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
+    }
+    {  // straight-line; weights: rsq/rcp Newton instead of the IEEE sqrt and divisions
+      const double len2 = dot(dir, dir);
+      const double dist2 = (t * t) * len2;
+      const double cosine = fabs(dot(dir, ld3(L, 0))) * rsq_nr(len2);
+      const double q = dist2 * rcp_w(cosine * ldd(L, 7));
+      pv = hq ? q : 0.0;
+    }
+  } else if (type == RTL_SPHERE) {
+    C.inc(RT_OP_LIGHT_PDF_SPHERE);
+    bool hs;
+    if (COUNT) {
+      double t = 0.0;
+      hs = sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C);
+    } else {
+      // Only a weight depends on this test (a PDF value), so the product build asks the same
+      // question without the root: some root of Sphere::hit lies in (0.001, inf) exactly when
+      // the far root does, (sqrt(disc) - half_b) / a > 0.001, i.e. sqrt(disc) > c1 = 0.001 a +
+      // half_b: true for c1 < 0, else disc > c1^2 (object.rs:145-166 at time 0, 193).
+      const d3 oc = origin - ld3(L, 0);
+      const double a = dot(dir, dir);
+      const double half_b = dot(oc, dir);
+      const double r = ldd(L, 3);
+      const double c = dot(oc, oc) - r * r;
+      const double disc = fma(half_b, half_b, -(a * c));
+      const double c1 = fma(0.001, a, half_b);
+      hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));
+    }
+    double cos_max = 0.0;
+    if ((int)i == P.sphere_light0) {  // uniform: the shared value (straight-line)
+      cos_max = cos_sl0;
+    } else if (hs) {
+      d3 cmo = ld3(L, 0) - origin;
+      double r = ldd(L, 3);
+      cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));
+    }
+    const double solid = 2.0 * kPi * (1.0 - cos_max);
+    const double q = rcp_w(solid);
+    pv = hs ? q : 0.0;
+  }
+  return pv;  // RTL_OTHER (Object::pdf_value's default arm, object.rs:306-311): 0
+}
+// A light entry: a leaf, or a HittableList nested inside the light list (RTL_LLIST, object.rs:66
+// -> hittable.rs:115-124): the left fold of its children's values times 1/len. NEST bounds the
+// nesting below this entry (the flattener rejects deeper light lists).
+template <bool COUNT, int NEST>
+__device__ double light_entry_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
+                                  double cos_sl0, Ctr<COUNT>& C) {
+  const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
+  if constexpr (NEST > 0) {
+    if ((L[0] & 0xffu) == RTL_LLIST) {
+      const uint32_t n = L[0] >> 8, first = L[1];
+      double sum = 0.0;
+      for (uint32_t k = 0; k < n; ++k) {
+        const double pv = light_entry_pdf<COUNT, NEST - 1>(P, first + k, origin, dir, cos_sl0, C);
+        sum = k == 0 ? pv : sum + pv;
+      }
+      return sum * ldd(L, 0);  // weight = 1 / len, the host's IEEE division
+    }
+  }
+  return light_leaf_pdf<COUNT>(P, i, origin, dir, cos_sl0, C);
+}
+template <bool COUNT>
 __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_sl0,
                             Ctr<COUNT>& C) {
   double sum = 0.0;
   for (uint32_t i = 0; i < P.n_lights; ++i) {
-    const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
-    uint32_t type = L[0] & 0xffu;
-    double pv = 0.0;
-    if (type == RTL_QUAD) {
-      C.inc(RT_OP_LIGHT_PDF_QUAD);
-      double t = 0.0;
-      bool hq;
-      const uint32_t axis = RTL_QUAD_AXIS(L[0]);
-      if (axis) {  // axis-aligned form at d24 (rt_layout.h): the world quads' bit-identical test
-        const kdptr A = reinterpret_cast<kdptr>(L + 4) + RTL_LQUAD_AXIS_D;
-        const AQuad q = {L[0], A[0], A[1], A[2], A[3], A[4]};
-        if (axis == 1u) {
-          hq = aquad_test<COUNT, 0>(q, origin, dir, mk(rcp_nr1(dir.x), 0., 0.), 0.001, kInf, t, C);
-        } else if (axis == 2u) {
-          hq = aquad_test<COUNT, 1>(q, origin, dir, mk(0., rcp_nr1(dir.y), 0.), 0.001, kInf, t, C);
-        } else {
-          hq = aquad_test<COUNT, 2>(q, origin, dir, mk(0., 0., rcp_nr1(dir.z)), 0.001, kInf, t, C);
-        }
-      } else {
-        hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
-      }
-      {  // straight-line; weights: rsq/rcp Newton instead of the IEEE sqrt and divisions
-        const double len2 = dot(dir, dir);
-        const double dist2 = (t * t) * len2;
-        const double cosine = fabs(dot(dir, ld3(L, 0))) * rsq_nr(len2);
-        const double q = dist2 * rcp_w(cosine * ldd(L, 7));
-        pv = hq ? q : 0.0;
-      }
-    } else if (type == RTL_SPHERE) {
-      C.inc(RT_OP_LIGHT_PDF_SPHERE);
-      bool hs;
-      if (COUNT) {
-        double t = 0.0;
-        hs = sphere_test<COUNT>(L, origin, dir, 0.0, 0.001, kInf, t, C);
-      } else {
-        // Only a weight depends on this test (a PDF value), so the product build asks the same
-        // question without the root: some root of Sphere::hit lies in (0.001, inf) exactly when
-        // the far root does, (sqrt(disc) - half_b) / a > 0.001, i.e. sqrt(disc) > c1 = 0.001 a +
-        // half_b: true for c1 < 0, else disc > c1^2 (object.rs:145-166 at time 0, 193).
-        const d3 oc = origin - ld3(L, 0);
-        const double a = dot(dir, dir);
-        const double half_b = dot(oc, dir);
-        const double r = ldd(L, 3);
-        const double c = dot(oc, oc) - r * r;
-        const double disc = fma(half_b, half_b, -(a * c));
-        const double c1 = fma(0.001, a, half_b);
-        hs = !(disc < 0.0) & ((c1 < 0.0) | (disc > c1 * c1));
-      }
-      double cos_max = 0.0;
-      if ((int)i == P.sphere_light0) {  // uniform: the shared value (straight-line)
-        cos_max = cos_sl0;
-      } else if (hs) {
-        d3 cmo = ld3(L, 0) - origin;
-        double r = ldd(L, 3);
-        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));
-      }
-      const double solid = 2.0 * kPi * (1.0 - cos_max);
-      const double q = rcp_w(solid);
-      pv = hs ? q : 0.0;
-    }
+    const double pv = P.lights_nested
+                          ? light_entry_pdf<COUNT, RTL_LIGHT_NEST>(P, i, origin, dir, cos_sl0, C)
+                          : light_leaf_pdf<COUNT>(P, i, origin, dir, cos_sl0, C);
     sum = i == 0 ? pv : sum + pv;
   }
   return P.lights_is_list ? sum * P.inv_n_lights : sum;  // weight = 1/len (hittable.rs:116)
@@ -1708,10 +1799,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (hf >= 0) {  // back to world space, innermost transform first
       uint4 fh = ld4u(T.nodes + hf);
       uint4 ch = ld4u(T.nodes + hf + 4);
-      const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
+      if (fh.x & RTL_XFORM_LONG) {
+        for (uint32_t k = fh.z; k-- > 0;) xform_out(T.nodes + T.nodes[ch.x + k], p, normal);
+      } else {
+        const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
 #pragma unroll
-      for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
-        if ((uint32_t)k < fh.z) xform_out(T.nodes + c4[k], p, normal);
+        for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
+          if ((uint32_t)k < fh.z) xform_out(T.nodes + c4[k], p, normal);
+      }
     }
     const uint32_t kind = mh.x & 0xffu;
     PROF(3);
@@ -1780,6 +1875,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
         L = T.lights + T.loffs[li];
         ltype = L[0] & 0xffu;
+        while (ltype == RTL_LLIST) {  // a nested HittableList: random_int pick (hittable.rs:126-129)
+          li = L[1] + rnd_index(g, L[0] >> 8);
+          L = T.lights + T.loffs[li];
+          ltype = L[0] & 0xffu;
+        }
       } else {
         C.inc(RT_OP_COSINE_GEN);
       }

@@ -34,6 +34,11 @@
 #define RTL_EXIT 6
 #define RTL_VOLUME 7
 #define RTL_OTHER 8 /* light entry whose pdf_value is 0 (Object default arm, object.rs:295-311) */
+#define RTL_LLIST 11 /* light table only: a HittableList nested in the light list (object.rs:57, 66):
+                       [hdr | count << 8][first entry][0][0] d0 = 1.0 / count; its children are
+                       the light entries [first, first + count) */
+#define RTL_LLIST_WORDS 8
+#define RTL_LIGHT_NEST 4 /* light lists nested at most this deep below the top-level list */
 #define RTL_QUADS 9 /* batch of consecutive sibling quads: header word 0 = type | count << 8, then
                        `count` QUAD records; traversed in order, exactly like the list it replaces */
 #define RTL_DUP 10  /* the right child of a BvhNode whose two children are the same deterministic
@@ -77,17 +82,22 @@
  *   obvh: word offset of the subtree's ordered BVH (below), 0 = none (walk the reference tree).
  * OBVH (rt_obvh.cpp), for a BVH subtree whose leaves are QUAD / QUADS / SPHERE records: an SAH
  * BVH2 over the same leaf records, appended after the record region (n_rec_words):
- *   [n_entries][n_boxes][boxes_off][streams_off]      (offsets in words from the OBVH header)
- *   boxes: n_boxes x 12 words, f64 xmin xmax ymin ymax zmin zmax (conservative: padded bounds)
- *   streams: 8 ray-direction octants (bit a set = d_a < 0) x n_entries x 2 words, each a
- *   threaded pre-order walk with the near child first: internal [skip][box] (box hit -> next
- *   entry, miss -> skip), leaf [0x80000000][record] (then the next entry). */
+ *   [n_entries][0][0][streams_off]                     (offset in words from the OBVH header)
+ *   streams: 8 ray-direction octants (bit a set = d_a < 0, by sign bit) x n_entries x 8 words,
+ *   each a threaded pre-order walk with the near child first. Internal entry:
+ *   [skip][0][near_x][far_x][near_y][far_y][near_z][far_z] (f32 bounds of the node's box for the
+ *   octant, outward-rounded with margin: box hit -> next entry, miss -> skip); leaf entry:
+ *   [0x80000000][record][0 x 6] (then the next entry). */
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
  *   translate: p = offset.xyz; rotate_y: p0 = sin, p1 = cos                  transform.rs */
 #define RTL_XFORM_WORDS 16
 #define RTL_MAX_CHAIN 4
+/* A chain longer than RTL_MAX_CHAIN (transform.rs nests without a limit): header flag
+ * RTL_XFORM_LONG, word 4 = word offset of the chain (chain_len words, root first) in a table
+ * appended after the records. */
+#define RTL_XFORM_LONG 0x100u
 /* EXIT (4 words): [hdr][skip=unused][parent frame node or -1][next] */
 #define RTL_EXIT_WORDS 4
 /* VOLUME header flags: the boundary is [Translate|RotateY]* then one sphere, or one batch (or
@@ -135,4 +145,5 @@ typedef struct rtl_scene_header {
   uint32_t volumes_one_walk_spheres; /* every ConstantMedium boundary is a one-walk sphere */
   uint32_t has_isotropic; /* some material is Isotropic (also outside a ConstantMedium)  */
   uint32_t n_rec_words;   /* node words holding records; ordered BVHs follow (OBVH below) */
+  uint32_t lights_nested; /* some light entry is a nested HittableList (RTL_LLIST)    */
 } rtl_scene_header;

@@ -20,6 +20,8 @@
 // the reference tree).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "rt_flatten.hpp"
@@ -106,6 +108,17 @@ struct Builder {
   }
 };
 
+float f32_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -HUGE_VALF);
+  return f;
+}
+float f32_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, HUGE_VALF);
+  return f;
+}
+
 // end of the record / subtree starting at x in the relocated array (the walker's continuation)
 bool subtree_end(const std::vector<uint32_t>& w, uint32_t x, uint32_t* end) {
   switch (w[x] & 0xffu) {
@@ -150,54 +163,57 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
     std::vector<Leaf> leaves;
     if (!collect(w, root, boxes, leaves, 0) || leaves.empty() || leaves.size() > (1u << 20))
       continue;
+    if (std::getenv("RT_OBVH_DEBUG")) {  // diagnostics: leaf count, distinct records
+      std::vector<uint32_t> r;
+      for (auto& l : leaves) r.push_back(l.rec);
+      std::sort(r.begin(), r.end());
+      std::fprintf(stderr, "obvh root %u: %zu leaves, %zu distinct\n", root, leaves.size(),
+                   (size_t)(std::unique(r.begin(), r.end()) - r.begin()));
+    }
     Builder B(leaves);
     B.build(0, (int)leaves.size(), 0);
-    // entries in pre-order; internal nodes own a box
+    // one stream of 8-word entries per ray-direction octant, in pre-order with the near child
+    // first; an internal entry carries its box as f32 (near, far) bound pairs for that octant
     const uint32_t n_entries = (uint32_t)B.nodes.size();
-    std::vector<int> box_of(B.nodes.size(), -1);
-    uint32_t n_boxes = 0;
-    for (size_t i = 0; i < B.nodes.size(); ++i)
-      if (B.nodes[i].left >= 0) box_of[i] = (int)n_boxes++;
     while (w.size() % 4) w.push_back(0u);
     const uint32_t hdr = (uint32_t)w.size();
-    const uint32_t boxes_off = 4, streams_off = boxes_off + n_boxes * 12;
-    w.resize(hdr + streams_off + 8 * n_entries * 2, 0u);
+    const uint32_t streams_off = 4;
+    w.resize(hdr + streams_off + (size_t)8 * n_entries * 8, 0u);
     w[hdr] = n_entries;
-    w[hdr + 1] = n_boxes;
-    w[hdr + 2] = boxes_off;
     w[hdr + 3] = streams_off;
-    for (size_t i = 0; i < B.nodes.size(); ++i) {
-      if (box_of[i] < 0) continue;
-      const BNode& n = B.nodes[i];
-      const double v[6] = {n.lo[0], n.hi[0], n.lo[1], n.hi[1], n.lo[2], n.hi[2]};
-      std::memcpy(&w[hdr + boxes_off + (size_t)box_of[i] * 12], v, sizeof v);
-    }
     for (uint32_t oct = 0; oct < 8; ++oct) {
-      uint32_t* S = &w[hdr + streams_off + (size_t)oct * n_entries * 2];
+      uint32_t* S = &w[hdr + streams_off + (size_t)oct * n_entries * 8];
       uint32_t pos = 0;
-      // pre-order with the near child first (recursion depth = tree depth <= kMaxDepth)
+      // pre-order with the near child first (recursion depth = tree depth <= kSahDepth + 20)
       struct Emit {
         const std::vector<BNode>& N;
-        const std::vector<int>& box_of;
         const std::vector<Leaf>& L;
         uint32_t* S;
         uint32_t oct;
         uint32_t& pos;
         void run(int i) {
           const BNode& n = N[i];
-          const uint32_t at = pos++;
+          uint32_t* E = S + (size_t)8 * pos++;
           if (n.left < 0) {
-            S[2 * at] = 0x80000000u;
-            S[2 * at + 1] = L[n.right].rec;
+            E[0] = 0x80000000u;
+            E[1] = L[n.right].rec;
             return;
           }
           const bool neg = (oct >> n.axis) & 1u;
           run(neg ? n.right : n.left);
           run(neg ? n.left : n.right);
-          S[2 * at] = pos;  // skip: the entry after the subtree
-          S[2 * at + 1] = (uint32_t)box_of[i];
+          E[0] = pos;  // skip: the entry after the subtree
+          for (int a = 0; a < 3; ++a) {
+            // conservative f32 bounds: the padded f64 box grown by 2^-18 (1 + |coord|) and
+            // rounded outwards (rt_kernel.h obvh_walk's error budget)
+            const double m = 0x1p-18 * (1.0 + std::max(std::fabs(n.lo[a]), std::fabs(n.hi[a])));
+            const float lo = f32_down(n.lo[a] - m), hi = f32_up(n.hi[a] + m);
+            const bool na = (oct >> a) & 1u;  // d_a < 0: the near bound is hi
+            std::memcpy(&E[2 + 2 * a], na ? &hi : &lo, 4);
+            std::memcpy(&E[3 + 2 * a], na ? &lo : &hi, 4);
+          }
         }
-      } em{B.nodes, box_of, leaves, S, oct, pos};
+      } em{B.nodes, leaves, S, oct, pos};
       em.run(0);
     }
     w[root + 3] = hdr;  // the reference BVH record points at its ordered tree

@@ -188,6 +188,7 @@ def load_device_lib(path: Path) -> C.CDLL:
                                      C.POINTER(RtStats)]),
         "rt_scene_layout_stats": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(C.c_uint32),
                                             C.c_int]),
+        "rt_scene_prof_counters": (C.c_int, [p, C.POINTER(C.c_uint64), C.c_int]),
         "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
                                         C.POINTER(C.c_int)]),
         "rt_scene_jit_info": (C.c_int, [p, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
@@ -486,6 +487,11 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
 
 LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
                 "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs"]
+
+
+def validate(blob: "Blob") -> int:
+    """rt_scene_validate: RT_OK, or raises RtError with the library's status and message."""
+    return _check_dev(device_lib().rt_scene_validate(blob.ref()))
 
 
 def layout_stats(blob: "Blob") -> dict:

@@ -498,3 +498,57 @@ def test_black_pixels_of_the_600_cornell_camera(gpu_available):
     black = int((rt.write_color(full, cam.samples_per_pixel).reshape(-1, 3).sum(1) == 0).sum())
     print(f"black pixels: {black} (book3.png: {m['black_pixels']})")
     assert abs(black - m["black_pixels"]) <= 0.002 * m["black_pixels"], black
+
+
+# ---------------------------------------------------------------- scene graphs the reference
+# accepts that round 1 rejected (rt_flatten.cpp)
+def test_nested_light_list_parity(gpu_available):
+    """A HittableList inside the light list (object.rs:57, 66 -> hittable.rs:115-129): the
+    mixture's light PDF folds the inner list's values times 1/len inside the outer fold, and a
+    light sample draws random_int twice (outer, then inner)."""
+    sc = rt.Scene(12)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    red = sc.lambertian((0.65, 0.05, 0.05))
+    light = sc.diffuse_light((9, 9, 9))
+    glass = sc.dielectric(1.5)
+    world = sc.hittable_list(
+        sc.quad((-5, 0, -5), (10, 0, 0), (0, 0, 10), white),
+        sc.quad((-5, 0, -3), (10, 0, 0), (0, 6, 0), red),
+        sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light),
+        sc.quad((2.5, 3, 0), (1, 0, 0), (0, 0, 1), light),
+        sc.sphere((0, 1, 1), 1.0, glass))
+    inner = sc.hittable_list(sc.sphere((0, 1, 1), 1.0, glass),
+                             sc.quad((2.5, 3, 0), (1, 0, 0), (0, 0, 1), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light), inner)
+    blob = sc.serialize(world, lights)
+    assert rt.layout_stats(blob)["lights"] == 2
+    cam = rt.camera_new(1.0, 64, 16, 20, 40, (0, 2.5, 9), (0, 1.5, 0), (0, 1, 0), 0, 0, (0, 0, 0))
+    state, msg = _jit_state(blob, cam)
+    assert state == 1, msg
+    _compare(blob, cam)
+
+
+def test_deep_transform_chain_parity(gpu_available):
+    """Translate / RotateY nested six deep (transform.rs:12-40 nests without a limit): the hit
+    record is replayed through the whole chain (rt_layout.h RTL_XFORM_LONG) in the interpreter
+    and in the scene-specialised walker, including EXIT back to a 5-deep parent frame."""
+    sc = rt.Scene(13)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    chk = sc.lambertian(tex=sc.checker_from_color(0.9, (0.9, 0.2, 0.1), (0.1, 0.3, 0.9)))
+    light = sc.diffuse_light((8, 8, 8))
+    obj = sc.hittable_list(sc.make_box((0, 0, 0), (0.8, 0.8, 0.8), chk),
+                           sc.sphere((0.4, 1.2, 0.4), 0.3, white))
+    for k in range(6):
+        obj = sc.rotate_y(obj, 12 + 5 * k) if k % 2 == 0 else sc.translate(obj, (0.1 * k, 0.05, -0.1))
+    obj = sc.hittable_list(obj, sc.sphere((1.5, 0.3, 0.5), 0.3, white))  # EXIT to a deep frame
+    for k in range(3):
+        obj = sc.translate(sc.rotate_y(obj, -7), (0.05, 0, 0.05))
+    world = sc.hittable_list(sc.quad((-4, -0.01, -4), (8, 0, 0), (0, 0, 8), white), obj,
+                             sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    state, msg = _jit_state(blob, cam := rt.camera_new(1.0, 64, 16, 20, 40, (0, 2.5, 7),
+                                                       (0.5, 0.5, 0), (0, 1, 0), 0, 0,
+                                                       (0.05, 0.05, 0.05)))
+    assert state == 1, msg
+    _compare(blob, cam)

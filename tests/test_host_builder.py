@@ -213,3 +213,23 @@ def test_presets_all_build():
         rt.preset_blob("nope")
     with pytest.raises(rt.RtError):
         rt.preset_blob("cornell_box", variant="nope")
+
+
+def test_scene_graphs_round1_rejected_now_validate():
+    """A nested light list and a 10-deep Translate/RotateY chain are valid reference inputs
+    (object.rs:57, 66; transform.rs): rt_scene_validate accepts them, an empty nested light list
+    is the reference's panic (hittable.rs:120) -> RT_ERR_EMPTY_LIGHTS."""
+    sc = rt.Scene(3)
+    white = sc.lambertian((0.7, 0.7, 0.7))
+    light = sc.diffuse_light((4, 4, 4))
+    obj = sc.sphere((0, 0, 0), 1.0, white)
+    for k in range(10):
+        obj = sc.translate(obj, (0.1, 0, 0)) if k % 2 else sc.rotate_y(obj, 10)
+    q = sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light)
+    world = sc.hittable_list(obj, q)
+    lights = sc.hittable_list(q, sc.hittable_list(sc.sphere((0, 0, 0), 1.0, white), q))
+    assert rt.validate(sc.serialize(world, lights)) == 0
+    bad = sc.hittable_list(q, sc.hittable_list())
+    with pytest.raises(rt.RtError) as e:
+        rt.validate(sc.serialize(world, bad))
+    assert e.value.code == rt.RT_ERR_EMPTY_LIGHTS
