@@ -1069,7 +1069,6 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
     // one (as the reference-order LANE walker)
     while (e < hd.x) {
       s = S[2 * e];
-      if (s.x & 0x80000000u) break;
       const uint4 s2 = S[2 * e + 1];
       const float tnx = (__uint_as_float(s.z) - ox) * ix, tfx = (__uint_as_float(s.w) - ox) * ix;
       const float tny = (__uint_as_float(s2.x) - oy) * iy, tfy = (__uint_as_float(s2.y) - oy) * iy;
@@ -1078,7 +1077,9 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
       const float tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
       const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
       const bool pass = fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
-      e = pass ? e + 1u : s.x;
+      const bool leaf = (s.x & 0x80000000u) != 0u;
+      if (leaf & pass) break;  // the leaf's own box is hit: test its record
+      e = (pass | leaf) ? e + 1u : s.x;
 #ifdef RT_PROF
       ++pf_box;
 #endif

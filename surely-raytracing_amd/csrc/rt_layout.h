@@ -87,7 +87,8 @@
  *   each a threaded pre-order walk with the near child first. Internal entry:
  *   [skip][0][near_x][far_x][near_y][far_y][near_z][far_z] (f32 bounds of the node's box for the
  *   octant, outward-rounded with margin: box hit -> next entry, miss -> skip); leaf entry:
- *   [0x80000000][record][0 x 6] (then the next entry). */
+ *   [0x80000000][record][the leaf's own box, as above] (box hit -> test the record; then the
+ *   next entry). */
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0

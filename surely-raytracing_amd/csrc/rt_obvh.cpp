@@ -197,13 +197,13 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
           if (n.left < 0) {
             E[0] = 0x80000000u;
             E[1] = L[n.right].rec;
-            return;
+          } else {
+            const bool neg = (oct >> n.axis) & 1u;
+            run(neg ? n.right : n.left);
+            run(neg ? n.left : n.right);
+            E[0] = pos;  // skip: the entry after the subtree
           }
-          const bool neg = (oct >> n.axis) & 1u;
-          run(neg ? n.right : n.left);
-          run(neg ? n.left : n.right);
-          E[0] = pos;  // skip: the entry after the subtree
-          for (int a = 0; a < 3; ++a) {
+          for (int a = 0; a < 3; ++a) {  // the node's (or leaf's) own box
             // conservative f32 bounds: the padded f64 box grown by 2^-18 (1 + |coord|) and
             // rounded outwards (rt_kernel.h obvh_walk's error budget)
             const double m = 0x1p-18 * (1.0 + std::max(std::fabs(n.lo[a]), std::fabs(n.hi[a])));
