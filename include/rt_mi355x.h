@@ -247,6 +247,17 @@ int rt_scene_trace_ms(rt_scene* scene, float* ms_out, int max_n, int* n_out);
  * the product build. */
 int rt_scene_prof_counters(rt_scene* scene, uint64_t* out, int n);
 
+/* Multi-GPU in ONE host process (no RCCL needed): the call's rows are dealt cyclically over
+ * devices[0..n_devices) (row r of the call -> device r mod n), every device renders
+ * its rows concurrently on its own stream, and the host buffer accum_rgb (opts->n_rows * W * 3)
+ * receives the de-interleaved frame. Bit for bit the image of rt_render on one device (the RNG
+ * is keyed by global pixel and sample). A device may be listed more than once. stats: samples,
+ * ms_total (= ms_kernel: host wall time), launches = n_devices. render_par_lights over N GPUs
+ * (render.rs:144-216). One process per GPU instead: rt_render_device on cyclic rows + an RCCL
+ * gather. */
+int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
+                    const int* devices, int n_devices, float* accum_rgb, rt_stats* stats);
+
 /* One-shot drop-in for render_par_lights: create + render + destroy. */
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
                    float* accum_rgb, rt_stats* stats);

@@ -723,6 +723,93 @@ int rt_render(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts, fl
   return rc;
 }
 
+int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
+                    const int* devices, int n_devices, float* accum, rt_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!blob || !cam || !opts || !devices || !accum || n_devices <= 0)
+    return set_err(RT_ERR_INVALID_ARG, "null argument or no devices");
+  if (opts->n_rows < 0 || opts->row_step <= 0 || cam->image_width <= 0)
+    return set_err(RT_ERR_INVALID_ARG, "bad row range");
+  const int W = cam->image_width, G = n_devices;
+  const size_t row_floats = (size_t)W * 3;
+  struct Part {
+    rt_scene* sc = nullptr;
+    hipStream_t stream = nullptr;
+    float* dbuf = nullptr;
+    std::vector<float> host;
+    rt_render_opts o{};
+  };
+  std::vector<Part> parts(G);
+  int rc = RT_OK;
+  auto cleanup = [&]() {
+    for (Part& p : parts) {
+      if (p.sc) (void)hipSetDevice(p.sc->device);
+      if (p.stream) (void)hipStreamSynchronize(p.stream);
+      if (p.dbuf) (void)hipFree(p.dbuf);
+      if (p.stream) (void)hipStreamDestroy(p.stream);
+      rt_scene_destroy(p.sc);
+    }
+  };
+  // device k renders rows k, k + G, ... of the call's rows (cyclic), each on its
+  // own stream; all devices run concurrently, the host only waits at the end
+  for (int k = 0; k < G && rc == RT_OK; ++k) {
+    Part& p = parts[k];
+    p.o = *opts;
+    p.o.row_begin = opts->row_begin + k * opts->row_step;
+    p.o.row_step = opts->row_step * G;
+    p.o.n_rows = k < opts->n_rows ? (opts->n_rows - k + G - 1) / G : 0;
+    p.o.device = devices[k];
+    if (p.o.n_rows == 0) continue;
+    rc = rt_scene_create(blob, devices[k], &p.sc);
+    if (rc != RT_OK) break;
+    hipError_t e = hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking);
+    const size_t n = (size_t)p.o.n_rows * row_floats;
+    if (e == hipSuccess) e = hipMalloc(&p.dbuf, n * sizeof(float));
+    if (e == hipSuccess && !(opts->flags & RT_FLAG_OVERWRITE)) {
+      p.host.resize(n);  // this device's rows of the caller's accumulator, accumulated on device
+      for (int j = 0; j < p.o.n_rows; ++j)
+        std::memcpy(&p.host[(size_t)j * row_floats],
+                    accum + (size_t)(k + (size_t)j * G) * row_floats, row_floats * sizeof(float));
+      e = hipMemcpyAsync(p.dbuf, p.host.data(), n * sizeof(float), hipMemcpyHostToDevice, p.stream);
+    }
+    if (e != hipSuccess) {
+      rc = set_err(RT_ERR_HIP, std::string("rt_render_multi setup: ") + hipGetErrorString(e));
+      break;
+    }
+    rc = rt_render_device(p.sc, cam, &p.o, p.dbuf, p.stream, nullptr);
+  }
+  for (int k = 0; k < G && rc == RT_OK; ++k) {
+    Part& p = parts[k];
+    if (!p.sc) continue;
+    const size_t n = (size_t)p.o.n_rows * row_floats;
+    p.host.resize(n);
+    hipError_t e = hipSetDevice(p.sc->device);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(p.host.data(), p.dbuf, n * sizeof(float), hipMemcpyDeviceToHost, p.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p.stream);
+    if (e != hipSuccess) {
+      rc = set_err(RT_ERR_HIP, std::string("rt_render_multi gather: ") + hipGetErrorString(e));
+      break;
+    }
+    for (int j = 0; j < p.o.n_rows; ++j)  // de-interleave into the caller's rows
+      std::memcpy(accum + (size_t)(k + (size_t)j * G) * row_floats, &p.host[(size_t)j * row_floats],
+                  row_floats * sizeof(float));
+  }
+  if (rc == RT_OK && stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    const int S = cam->sqrt_spp, n_sj = opts->sj_count > 0 ? opts->sj_count : S;
+    stats->samples = (uint64_t)opts->n_rows * W * (uint64_t)n_sj * S;
+    stats->ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->ms_kernel = stats->ms_total;
+    stats->launches = (uint32_t)G;
+  }
+  const std::string err = rc == RT_OK ? std::string() : g_err;
+  cleanup();
+  if (rc != RT_OK) g_err = err;
+  return rc;
+}
+
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
                    float* accum, rt_stats* stats) {
   if (!opts) return set_err(RT_ERR_INVALID_ARG, "null opts");

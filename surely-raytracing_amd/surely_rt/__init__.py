@@ -189,6 +189,9 @@ def load_device_lib(path: Path) -> C.CDLL:
         "rt_scene_layout_stats": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(C.c_uint32),
                                             C.c_int]),
         "rt_scene_prof_counters": (C.c_int, [p, C.POINTER(C.c_uint64), C.c_int]),
+        "rt_render_multi": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(RtCamera),
+                                      C.POINTER(RtRenderOpts), C.POINTER(C.c_int), C.c_int,
+                                      C.c_void_p, C.POINTER(RtStats)]),
         "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
                                         C.POINTER(C.c_int)]),
         "rt_scene_jit_info": (C.c_int, [p, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
@@ -487,6 +490,19 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
 
 LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
                 "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs"]
+
+
+def render_multi(blob: "Blob", cam: RtCamera, opts: RtRenderOpts, devices,
+                 accum: np.ndarray | None = None):
+    """rt_render_multi: the call's rows dealt cyclically over `devices` (one process, N GPUs),
+    gathered into one host frame. Returns (accum [n_rows, W, 3] float32, RtStats)."""
+    devs = (C.c_int * len(devices))(*devices)
+    if accum is None:
+        accum = np.zeros((opts.n_rows, cam.image_width, 3), np.float32)
+    st = RtStats()
+    _check_dev(device_lib().rt_render_multi(blob.ref(), C.byref(cam), C.byref(opts), devs,
+                                            len(devices), accum.ctypes.data, C.byref(st)))
+    return accum, st
 
 
 def validate(blob: "Blob") -> int:

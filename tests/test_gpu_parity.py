@@ -552,3 +552,23 @@ def test_deep_transform_chain_parity(gpu_available):
                                                        (0.05, 0.05, 0.05)))
     assert state == 1, msg
     _compare(blob, cam)
+
+
+def test_render_multi_devices_bitwise(gpu_available):
+    """rt_render_multi (one process, N devices, cyclic rows, host de-interleave): with the box's
+    one GPU listed 2 and 3 times it must give the single-device frame bit for bit, also when
+    accumulating into a non-zero buffer."""
+    blob, cam = rt.preset_blob("cornell_box", width=72, spp=16)
+    ds = rt.DeviceScene(blob)
+    full, _ = ds.render(cam, rt.make_opts(cam, seed=4))
+    base = np.random.default_rng(1).random(full.shape, dtype=np.float32)
+    acc_one = base.copy()
+    ds.render(cam, rt.make_opts(cam, seed=4, flags=0), accum=acc_one)
+    ds.close()
+    for devs in ([0, 0], [0, 0, 0]):
+        got, st = rt.render_multi(blob, cam, rt.make_opts(cam, seed=4), devs)
+        assert np.array_equal(got, full), devs
+        assert st.samples == 72 * 72 * 16 and st.launches == len(devs)
+        acc = base.copy()
+        rt.render_multi(blob, cam, rt.make_opts(cam, seed=4, flags=0), devs, accum=acc)
+        assert np.array_equal(acc, acc_one), devs

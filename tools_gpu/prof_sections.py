@@ -1,7 +1,11 @@
 """Wave-cycle split of the path loop by section (build/prof, -DRT_PROF; not shipped).
 Usage: python tools_gpu/prof_sections.py [scene width spp]"""
 import ctypes as C
+import os
 import sys
+
+if os.environ.get("AB_TORCH", "1") == "1":
+    import torch  # noqa: F401  (as bench.py: torch's bundled hiprtc builds the scene kernels)
 
 sys.path.insert(0, "surely-raytracing_amd")
 import numpy as np  # noqa: E402
