@@ -40,10 +40,10 @@ namespace {
 
 // Ahead-of-time kernels: the interpreter traversal, one per feature combination.
 template <bool COUNT, bool VOL, bool TEX, bool BVH, bool STAGED, bool VOLB = VOL,
-          bool VOLI = true>
+          bool VOLI = true, int VN = 0>
 __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::value)) void rt_trace(
     TraceParams P) {
-  trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterp>(P);
+  trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterpN<VN>>(P);
 }
 
 // Per pixel: the f64 sum of each stratum row s_j (a row item's partial, or the sequential s_i
@@ -482,7 +482,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
       rt_trace<false, true, false, false, true>,  rt_trace<false, true, true, false, true>,
       rt_trace<true, false, false, false, true>,  rt_trace<true, false, true, false, true>,
       rt_trace<true, true, false, false, true>,   rt_trace<true, true, true, false, true>};
-  const bool staged = !bvh && P.stage_scene;
+  const bool staged = !bvh && P.stage_scene && !sc->hdr.nested_volumes;
   const int kidx = ((opts->flags & RT_FLAG_COUNT_OPS) ? 8 : 0) + (vol ? 4 : 0) + (tex ? 2 : 0) +
                    (bvh ? 1 : 0) + (staged ? 16 : 0);
   // BVH scenes whose volumes all sit outside BVH subtrees (final_scene) run the variant whose
@@ -501,6 +501,18 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int vb = (novoli ? 4 : 0) + (kidx >= 8 ? 2 : 0) + (tex ? 1 : 0);
   kern_t kern = staged ? table_staged[kidx / 2 - 8] : (novolb ? table_bvh_novolb[vb] : table[kidx]);
   int kslot = novolb ? 32 + vb : kidx;
+  // ConstantMedium nested in volume boundaries (rt_flatten.cpp: at most RTL_VOLUME_NEST deep):
+  // the generic texture/volume kernels that walk them (no scene-specialised kernel)
+  static const kern_t table_nested[4] = {
+      rt_trace<false, true, true, false, false, true, true, RTL_VOLUME_NEST>,
+      rt_trace<false, true, true, true, false, true, true, RTL_VOLUME_NEST>,
+      rt_trace<true, true, true, false, false, true, true, RTL_VOLUME_NEST>,
+      rt_trace<true, true, true, true, false, true, true, RTL_VOLUME_NEST>};
+  if (sc->hdr.nested_volumes) {
+    const int ni = ((opts->flags & RT_FLAG_COUNT_OPS) ? 2 : 0) + (bvh ? 1 : 0);
+    kern = table_nested[ni];
+    kslot = 44 + ni;
+  }
   hipFunction_t jfn = nullptr;
   if (want_jit && lds_bytes + static_lds <= sc->lds_module_max) {
     rtj::Kernel& jk = sc->jit_k[(tex ? 1 : 0) + (staged ? 2 : 0)];

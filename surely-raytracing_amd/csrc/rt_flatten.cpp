@@ -147,6 +147,7 @@ struct Emitter {
   int status = RT_OK;
   uint32_t max_chain = 0;
   bool has_bvh = false, has_volume = false, volume_in_bvh = false, all_sphere_volumes = true;
+  bool nested_volumes = false;
   int bvh_depth = 0;  // BVH subtrees enclosing the record being emitted
   size_t last_exit_end = (size_t)-1;  // end position of the most recent EXIT node
   size_t last_skip_target = (size_t)-1;
@@ -317,7 +318,7 @@ struct Emitter {
     w[p + 2] = (uint32_t)parent;
     last_exit_end = w.size();
   }
-  void emit(const Node& n, int frame, std::vector<uint32_t>& chain, bool in_volume) {
+  void emit(const Node& n, int frame, std::vector<uint32_t>& chain, int in_volume) {
     if (status != RT_OK) return;
     switch (n.tag) {
       case RT_OBJ_LIST: {
@@ -397,17 +398,23 @@ struct Emitter {
         break;
       }
       case RT_OBJ_VOLUME: {
-        if (in_volume) {
-          fail(RT_ERR_UNSUPPORTED, "ConstantMedium nested inside a ConstantMedium boundary");
+        if (in_volume > RTL_VOLUME_NEST) {
+          fail(RT_ERR_UNSUPPORTED, "ConstantMedium boundaries nested deeper than " +
+                                       std::to_string(RTL_VOLUME_NEST));
           return;
         }
+        if (in_volume > 0 && bvh_depth > 0) {
+          fail(RT_ERR_UNSUPPORTED, "ConstantMedium inside a BVH inside a ConstantMedium boundary");
+          return;
+        }
+        if (in_volume > 0) nested_volumes = true;
         if (!check_mat(n.mat)) return;
         has_volume = true;
         if (bvh_depth > 0) volume_in_bvh = true;
         size_t p = push(RTL_VOLUME, RTL_VOLUME_WORDS);
         w[p + 2] = (uint32_t)n.mat;
         putd(w, p, 0, n.f[0]);
-        emit(*n.kids[0], frame, chain, true);
+        emit(*n.kids[0], frame, chain, in_volume + 1);
         push(RTL_END, RTL_END_WORDS);
         set_skip(p);
         w[p] |= fusable_boundary(p + RTL_VOLUME_WORDS);
@@ -677,7 +684,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   }
   Emitter em(F.nodes, (int64_t)n_mat);
   std::vector<uint32_t> chain;
-  em.emit(*world, -1, chain, false);
+  em.emit(*world, -1, chain, 0);
   em.push(RTL_END, RTL_END_WORDS);
   if (em.status != RT_OK) {
     *err = em.err;
@@ -783,6 +790,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.n_lights = n_lights;
   h.lights_is_list = is_list;
   h.lights_nested = lights_nested;
+  h.nested_volumes = em.nested_volumes;
   h.has_bvh = em.has_bvh;
   h.has_volume = em.has_volume;
   h.volume_in_bvh = em.volume_in_bvh;

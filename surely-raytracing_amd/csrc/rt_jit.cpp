@@ -332,6 +332,10 @@ bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string*
 
 std::string generate(const rtf::FlatScene& F, std::string* why) {
   const std::vector<uint32_t>& N = F.nodes;
+  if (F.hdr.nested_volumes) {
+    *why = "ConstantMedium nested in a volume boundary: the interpreter kernel walks it";
+    return "";
+  }
   if (N.size() > kMaxWords) {
     *why = "node array too large for the packed winner code";
     return "";

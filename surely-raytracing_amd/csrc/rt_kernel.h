@@ -715,7 +715,10 @@ __device__ __forceinline__ bool prof_first_lane() {
 // branch, a nested walker; without it the LANE instantiation leaves that code out).
 // VOLI: some ConstantMedium boundary may need the interpreter's two walks (not one-walk, or one-
 // walk quads whose third candidate can be needed); without it only volume_two_hits is compiled.
-template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL, bool VOLI = true>
+// VN: ConstantMedium records nested inside volume boundaries are handled this many levels deep
+// (constant_medium.rs:46-55 queries `boundary.hit`, which may be another ConstantMedium).
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB = VOL, bool VOLI = true,
+          int VN = 0>
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
                          double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
@@ -724,7 +727,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
 // current frame (o, d): true when the free-flight distance ends inside the boundary before
 // `closest`, with the hit t in t_hit. Shared by the interpreter walker and the generated
 // walkers of rt_jit.cpp.
-template <bool COUNT, bool UNI, bool BVH, bool VOLI, class VT = VolTwoInterp>
+template <bool COUNT, bool UNI, bool BVH, bool VOLI, class VT = VolTwoInterp, int VN = 0>
 __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, uint4 h, d3 wo,
                                            d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                                            double closest, double& t_hit, Rng& g, Ctr<COUNT>& C) {
@@ -760,10 +763,12 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
       double tb;
       uint32_t dn;
       int df;
-      both = traverse<false, COUNT, false, UNI, BVH>(P, h.w, ~0u, wo, wd, tm,
-                                                     o, d, frame,
-                                                     pass ? t1 + 0.0001 : -kInf, kInf,
-                                                     tb, dn, df, g, C);
+      // a boundary holding ConstantMedium records (VN > 0) walks them too: their hits (and
+      // random draws) are part of `boundary.hit`, in the reference's order
+      both = traverse<false, COUNT, (VN > 0), UNI, BVH, false, true, VN>(P, h.w, ~0u, wo, wd, tm,
+                                                                         o, d, frame,
+                                                                         pass ? t1 + 0.0001 : -kInf,
+                                                                         kInf, tb, dn, df, g, C);
       if (pass) t2 = tb; else t1 = tb;
     }
   }
@@ -793,7 +798,7 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
                             Rng& g, Ctr<COUNT>& C);
 
-template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB, bool VOLI>
+template <bool MAIN, bool COUNT, bool VOL, bool UNI, bool BVH, bool VOLB, bool VOLI, int VN>
 __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 wo, d3 wd,
                          double tm, d3 o, d3 d, int frame, double tmin, double tmax,
                          double& t_out, uint32_t& hit_node, int& hit_frame, Rng& g,
@@ -984,14 +989,16 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
       frame_ray(N, frame, wo, wd, o, d);
       if (!UNI) inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
       node = h.w;
-    } else if (MAIN && VOL && type == RTL_VOLUME) {
+    } else if ((MAIN || VN > 0) && VOL && type == RTL_VOLUME) {
       double tv;
-      if (volume_hit<COUNT, UNI, BVH, VOLI>(P, node, h, wo, wd, tm, o, d, frame, tmin, closest, tv,
-                                            g, C)) {
+      if (volume_hit<COUNT, UNI, BVH, VOLI, VolTwoInterp, (MAIN ? VN : (VN > 0 ? VN - 1 : 0))>(
+              P, node, h, wo, wd, tm, o, d, frame, tmin, closest, tv, g, C)) {
         closest = tv;
         hit = true;
-        hit_node = node;
-        hit_frame = frame;
+        if (MAIN) {
+          hit_node = node;
+          hit_frame = frame;
+        }
       }
       node = h.y;
     } else if (type == RTL_DUP) {
@@ -1484,13 +1491,16 @@ __device__ __forceinline__ d3 xs_resolve(d3 L, uint32_t xs) {
 // The world query of ray_color (render.rs:267: world.hit(r, Interval(0.001 -> 1e-4, inf))), by
 // the run-time interpreter of the flattened node sequence. Scene-specialised kernels (rt_jit.cpp)
 // supply a generated policy with the same signature and the same arithmetic.
-struct TravInterp {
+// VN > 0: the scene nests ConstantMedium records inside volume boundaries (that deep).
+template <int VN>
+struct TravInterpN {
   template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>
   static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,
                                                double& t, uint32_t& hn, int& hf, Rng& g,
                                                Ctr<COUNT>& C) {
-    return traverse<true, COUNT, VOL, true, BVH, VOLB, VOLI>(P, P.root, ~0u, ro, rd, tm, ro, rd,
-                                                             -1, 0.0001, kInf, t, hn, hf, g, C);
+    return traverse<true, COUNT, VOL, true, BVH, VOLB, VOLI, VN>(P, P.root, ~0u, ro, rd, tm, ro,
+                                                                 rd, -1, 0.0001, kInf, t, hn, hf,
+                                                                 g, C);
   }
   // the mixture's light-list PDF value (pdf.rs:91-93)
   template <bool COUNT>
@@ -1499,6 +1509,7 @@ struct TravInterp {
     return light_pdf<COUNT>(P, origin, dir, cos_sl0, C);
   }
 };
+typedef TravInterpN<0> TravInterp;
 
 // The path kernel body; instantiated by rt_device.hip (interpreter) and by scene-specialised
 // JIT kernels. Its __global__ wrapper passes TraceParams as the only kernel argument (kparams()).

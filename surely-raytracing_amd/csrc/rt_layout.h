@@ -110,6 +110,9 @@
 /* VOLUME (8 words): [hdr][skip][mat][next] d0 neg_inv_density, d1 0; the boundary follows and an
  * END node terminates it                                                    constant_medium.rs */
 #define RTL_VOLUME_WORDS 8
+/* ConstantMedium records nested inside volume boundaries (constant_medium.rs:46-55 queries
+ * `boundary.hit`, which may itself hold a ConstantMedium): walked at most this deep */
+#define RTL_VOLUME_NEST 2
 #define RTL_END_WORDS 4
 
 /* material (20 words): [kind | flags(bit8: texture reads uv)][tex][0][0] d0-3 c.xyz, param,
@@ -147,4 +150,5 @@ typedef struct rtl_scene_header {
   uint32_t has_isotropic; /* some material is Isotropic (also outside a ConstantMedium)  */
   uint32_t n_rec_words;   /* node words holding records; ordered BVHs follow (OBVH below) */
   uint32_t lights_nested; /* some light entry is a nested HittableList (RTL_LLIST)    */
+  uint32_t nested_volumes;/* a ConstantMedium lies inside another one's boundary      */
 } rtl_scene_header;

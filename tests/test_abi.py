@@ -74,14 +74,19 @@ def test_validate_rejects_out_of_range_material():
     assert lib.rt_scene_validate(rt.Blob(slots, blob.texels).ref()) == rt.RT_ERR_BAD_BLOB
 
 
-def test_unsupported_nesting_reported():
-    """A ConstantMedium whose boundary contains another ConstantMedium is valid Rust but the
-    device traversal keeps one boundary sub-walk: rejected with RT_ERR_UNSUPPORTED."""
+def test_nested_constant_medium_depth_limit():
+    """ConstantMedium boundaries may hold ConstantMedium records (constant_medium.rs:46-55);
+    the device walks them RTL_VOLUME_NEST = 2 levels deep and reports a deeper nesting as
+    RT_ERR_UNSUPPORTED instead of rendering it wrongly."""
     sc = rt.Scene(1)
-    inner = sc.constant_medium(sc.sphere((0, 0, 0), 1, sc.dielectric(1.5)), 0.5, (1, 1, 1))
-    outer = sc.constant_medium(sc.hittable_list(inner), 0.5, (1, 1, 1))
-    blob = sc.serialize(sc.hittable_list(outer))
-    assert rt.device_lib().rt_scene_validate(blob.ref()) == rt.RT_ERR_UNSUPPORTED
+    glass = sc.dielectric(1.5)
+    vol = sc.constant_medium(sc.sphere((0, 0, 0), 1, glass), 0.5, (1, 1, 1))
+    for depth in range(1, 4):
+        vol = sc.constant_medium(sc.hittable_list(sc.sphere((0, 0, 0), 1 + depth, glass), vol),
+                                 0.5, (1, 1, 1))
+        blob = sc.serialize(sc.hittable_list(vol))
+        want = rt.RT_OK if depth <= 2 else rt.RT_ERR_UNSUPPORTED
+        assert rt.device_lib().rt_scene_validate(blob.ref()) == want, depth
 
 
 def test_product_path_fails_loudly_without_library(tmp_path):

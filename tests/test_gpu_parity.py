@@ -572,3 +572,24 @@ def test_render_multi_devices_bitwise(gpu_available):
         acc = base.copy()
         rt.render_multi(blob, cam, rt.make_opts(cam, seed=4, flags=0), devs, accum=acc)
         assert np.array_equal(acc, acc_one), devs
+
+
+def test_nested_constant_medium_parity(gpu_available):
+    """A ConstantMedium whose boundary holds another ConstantMedium (constant_medium.rs:46-55:
+    `boundary.hit` is the inner medium's hit, with its own random draw per query), two levels
+    deep, in the reference's draw order."""
+    sc = rt.Scene(14)
+    white = sc.lambertian((0.73, 0.73, 0.73))
+    light = sc.diffuse_light((8, 8, 8))
+    inner = sc.constant_medium(sc.sphere((0, 1, 0), 0.6, white), 3.0, (0.9, 0.3, 0.2))
+    mid = sc.constant_medium(sc.hittable_list(sc.sphere((0, 1, 0), 1.0, white), inner), 1.5,
+                             (0.2, 0.5, 0.9))
+    outer = sc.constant_medium(sc.hittable_list(sc.sphere((0, 1, 0), 1.4, white), mid), 0.6,
+                               (0.8, 0.8, 0.8))
+    world = sc.hittable_list(sc.quad((-4, -0.01, -4), (8, 0, 0), (0, 0, 8), white), outer,
+                             sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 4, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 64, 16, 20, 40, (0, 2, 6), (0, 1, 0), (0, 1, 0), 0, 0, (0.05, 0.05, 0.05))
+    acc_g, _, st = _compare(blob, cam)
+    assert st.op_counts()["volume_draws"] > 0
