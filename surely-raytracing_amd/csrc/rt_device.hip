@@ -350,7 +350,8 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   auto t0 = std::chrono::steady_clock::now();
   if (!sc || !cam || !opts || !accum) return set_err(RT_ERR_INVALID_ARG, "null argument");
   const int W = cam->image_width, S = cam->sqrt_spp;
-  if (W <= 0 || cam->image_height <= 0 || S <= 0 || cam->max_depth < 0 || opts->n_rows < 0 ||
+  if (W <= 0 || cam->image_height <= 0 || S <= 0 || cam->max_depth < 0 ||
+      cam->max_depth > 0xffffff || opts->n_rows < 0 ||
       opts->row_step <= 0 || opts->row_begin < 0)
     return set_err(RT_ERR_INVALID_ARG, "bad camera or row range");
   if (opts->n_rows > 0 &&

@@ -1593,7 +1593,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   const int lane = threadIdx.x & 63;
   int q = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_jp = 0;
   bool tailp = false;  // the pool is a tail pool (one item per sample)
-  uint32_t out0 = 0;   // tail pools: output index of (s_i = 0, pv = 0)
   bool more = true;    // the queue may still hold pools
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
@@ -1604,26 +1603,34 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 
   d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
   double tm = 0.;
+  // remaining bounces (low 24 bits, render.rs:260) | special-value state RT_XS_* << 24
   int depth = 0;
   bool alive = false;  // a path is in flight
   bool fresh = false;  // the lane's next sample needs its camera ray (claimed item / next s_i)
   uint32_t xk = 0;     // x | row-in-call << 16 | tail item << 31
   uint32_t sij = 0;    // s_j << 16 | s_i of the sample in flight
-  uint32_t outi = 0;   // output index of the item (TraceParams::part)
-  uint32_t xs = 0;     // special-value state of the path (RT_XS_*)
   int next = 0;        // pool items claimed so far (wave-uniform)
   Rng g = {0u, 0u, 0u, 0u};
   // A sample's radiance is final: add it to the item's running sum; a row item continues with
   // its next s_i, a finished item writes its f64 sum.
   auto end_sample = [&](d3 L) {
-    L = xs_resolve(L, xs);
+    L = xs_resolve(L, (uint32_t)depth >> 24);
     double a0 = sh_acc[tid] + L.x, a1 = sh_acc[NB + tid] + L.y, a2 = sh_acc[2 * NB + tid] + L.z;
     alive = false;
     if (!(xk >> 31) && (int)(sij & 0xffffu) + 1 < P.sqrt_spp) {
       sh_acc[tid] = a0, sh_acc[NB + tid] = a1, sh_acc[2 * NB + tid] = a2;
       sij += 1u;
       fresh = true;
-    } else {
+    } else {  // the item's output index (TraceParams::part), from its pixel and stratum
+      const int x = (int)(xk & 0xffffu), kr = (int)((xk >> 16) & 0x7fffu);
+      const int tx = x >> 3, tw = imin(kWaveTile, P.W - tx * kWaveTile);
+      const uint32_t pv = (uint32_t)((kr & 7) * tw + (x & 7));
+      const uint32_t qq = (uint32_t)((kr >> 3) * P.tiles_x + tx) * (uint32_t)P.n_sj +
+                          ((sij >> 16) - (uint32_t)P.sj0);
+      const uint32_t outi =
+          (xk >> 31) ? ((uint32_t)P.n_pairs_a + (qq - (uint32_t)P.n_pairs_a) * (uint32_t)P.sqrt_spp +
+                        (sij & 0xffffu)) * 64u + pv
+                     : qq * 64u + pv;
       double* o = P.part + (size_t)outi * 3;
       o[0] = a0, o[1] = a1, o[2] = a2;
     }
@@ -1647,7 +1654,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
           const int qb = b / P.n_blk;
           blk = b - qb * P.n_blk;
           q = P.n_pairs_a + qb;
-          out0 = (uint32_t)P.n_pairs_a * 64u + (uint32_t)qb * (uint32_t)P.sqrt_spp * 64u;
         } else {
           q = (int)id;
         }
@@ -1683,7 +1689,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         const int kr = ty * kWaveTile + pv / tile_w;
         xk = (uint32_t)x | (uint32_t)kr << 16 | (tailp ? 0x80000000u : 0u);
         sij = (uint32_t)s_jp << 16 | (uint32_t)s_i;
-        outi = tailp ? out0 + (uint32_t)s_i * 64u + (uint32_t)pv : (uint32_t)q * 64u + (uint32_t)pv;
         sh_acc[tid] = 0.0, sh_acc[NB + tid] = 0.0, sh_acc[2 * NB + tid] = 0.0;
         fresh = true;
       }
@@ -1719,8 +1724,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       tm = rnd(g);
       beta = mk(1., 1., 1.);
       Lp = mk(0., 0., 0.);
-      depth = P.max_depth;
-      xs = 0u;
+      depth = P.max_depth;  // RT_XS_* cleared
       alive = true;
       fresh = false;
     }
@@ -1733,7 +1737,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // cut-off, miss, light); the ending lanes of all three kinds then share ONE end_sample.
     bool term = false;
     do {
-    if (depth <= 0) {  // ray_color depth guard render.rs:260-262
+    if ((depth & 0xffffff) == 0) {  // ray_color depth guard render.rs:260-262
       C.inc(RT_OP_DEPTH_CUTOFF);
       term = true;
       break;
@@ -1968,7 +1972,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       factor = atten * (s_pdf * rcp_w(pdf_val));
 #ifndef RT_ABL_NOXS  // ablation build: no special-value tracking (cost of RT_XS_*)
       if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
-        xs |= RT_XS_ON | xs_nan_bits(atten * s_pdf, beta);
+        depth |= (int)((RT_XS_ON | xs_nan_bits(atten * s_pdf, beta)) << 24);
         Lp = mk(0., 0., 0.);
         beta = mk(1., 1., 1.);
         factor = beta;
