@@ -1,10 +1,12 @@
 """Strong-scaling probe on one GPU: time one rank's cyclic share (rows r::N) vs the full frame.
 efficiency(N) ~= T_full / (N * max_r T_share(r)). Usage: python tools_gpu/scaling_probe.py [W spp]"""
+import os
 import sys
+if os.environ.get("AB_TORCH", "1") == "1":
+    import torch  # noqa: F401  (as bench.py: torch's bundled hiprtc builds the scene kernels)
 sys.path.insert(0, "surely-raytracing_amd")
 import numpy as np  # noqa: E402
 import surely_rt as rt  # noqa: E402
-import os  # noqa: E402
 
 if os.environ.get("RT_LIB"):  # a library variant (tools only)
     rt._dev = rt.load_device_lib(os.environ["RT_LIB"])
@@ -12,7 +14,8 @@ from surely_rt.parallel import cyclic_rows  # noqa: E402
 
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 800
 SPP = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
-blob, cam = rt.preset_blob("cornell_box", width=W, spp=SPP)
+SCENE = sys.argv[3] if len(sys.argv) > 3 else "cornell_box"
+blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
 ds = rt.DeviceScene(blob)
 H = cam.image_height
 
