@@ -65,7 +65,7 @@ variants: $(DEV_SRC) $(DEV_HDR)
 # VARDIR=build/variants_occ python tools_gpu/ab_variants.py W SPP ROUNDS SCENE
 variants-occ: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_occ
-	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=3 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh3.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=2 -DRT_BLOCK_BVH=512 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh2.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES_BVH=4 -shared $(DEV_SRC) -o $(BUILD)/variants_occ/librtmi355x_bvh4.so -lhiprtc
 
 # section-cycle profiling build (tools_gpu/prof_sections.py); not shipped

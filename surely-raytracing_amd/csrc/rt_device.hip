@@ -465,6 +465,9 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
   const int n_tiles = P.tiles_x * tiles_y;
   P.n_blk = (S + kPoolSi - 1) / kPoolSi;
+  P.regen_min = kRegenMin;
+  if (const char* e = std::getenv("RT_REGEN_MIN")) P.regen_min = std::atoi(e);  // A/B only
+  P.regen_min = std::max(1, std::min(64, P.regen_min));
   typedef void (*kern_t)(TraceParams);
   // [count][vol][tex][bvh]; a scene without a BVH whose tables are staged in LDS runs the
   // STAGED variant (LDS-typed table reads), BVH kernels read the tables from global memory

@@ -42,6 +42,8 @@ constexpr int kWaveTile = 8;  // 8x8 pixels per wave
 #define RT_POOL_SI 8
 #endif
 constexpr int kPoolSi = RT_POOL_SI;
+// Lanes that must wait before a wave generates their camera rays together (TraceParams::regen_min)
+constexpr int kRegenMin = 1;
 constexpr int kBlock = 256;   // 4 waves per workgroup
 // BVH kernels run three waves per SIMD (MinWaves below: <= 168 VGPRs) in ONE 768-thread
 // workgroup per CU, so the workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH
@@ -253,6 +255,7 @@ struct TraceParams {
   int W, n_rows, row_begin, row_step, sqrt_spp, sj0, n_sj, max_depth;
   uint32_t seed_lo, seed_hi;
   int tiles_x;
+  int regen_min;  // camera rays of waiting lanes are generated once this many lanes wait (§4.1)
 };
 
 // The kernel's only argument sits at offset 0 of the kernarg segment. Camera constants are read
@@ -1694,7 +1697,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       }
     }
     next += __popcll(want);
-    if (fresh) {
+    // Camera rays for the lanes waiting on one (claimed items, next s_i) are generated together
+    // once regen_min lanes wait, or when no path is in flight: the block then runs at a higher
+    // lane utilisation. A sample's arithmetic does not depend on when it starts.
+    const unsigned long long wf = __ballot(fresh);
+    if (wf != 0ull && (__popcll(wf) >= P.regen_min || __ballot(alive) == 0ull) && fresh) {
       const kparams_t Q = kparams();
       const int x = (int)(xk & 0xffffu);
       const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
