@@ -7,16 +7,15 @@
 // Material scatter (material.rs:92-248), PDFs (pdf.rs:44-127), Onb (onb.rs:24-47), textures
 // and Perlin noise (texture.rs:17-131, perlin.rs:30-96), vec3 math (vec3.rs).
 //
-// Work decomposition: a wave owns a POOL = one 8x8 pixel tile x one stratum row
-// s_j x all sqrt_spp samples s_i of that row (64 x 31 paths for 961 spp). Each lane traces one
-// path at a time (ray_color's recursion -> an iterative bounce loop with beta/L); when it
-// terminates, the lane stores the sample's radiance and claims the next pool item with a wave
-// ballot + mbcnt, so lanes stay busy until the pool drains whatever the per-pixel path cost.
-// The first 64 items are s_i = 0 for every pixel of the tile: camera rays and first hits are
-// coherent. Samples land in a per-sample slot; rt_reduce sums them in the reference's order
-// (s_i inside s_j, render.rs:185-189) into the caller's accumulator, so no atomics touch the
-// framebuffer and results are bitwise reproducible and identical across 1..8 GPUs (the RNG is
-// keyed by global pixel and sample).
+// Work decomposition: persistent waves claim POOLS from a global queue; a pool
+// is one 8x8 pixel tile x one stratum row s_j x one block of kPoolSi stratum columns s_i. Each
+// lane traces one path at a time (ray_color's recursion -> an iterative bounce loop with beta/L)
+// and takes a segment item (one pixel's samples of the block, summed in f64 in LDS) or, for the
+// launch's last pools, one sample; when its item ends it writes the f64 partial and claims the
+// next item with a wave ballot + mbcnt, so lanes stay busy whatever the per-pixel path cost.
+// rt_reduce sums the partials in the reference's order (s_i inside s_j, render.rs:185-189) into
+// the caller's accumulator, so no atomics touch the framebuffer and results are bitwise
+// reproducible and identical across 1..8 GPUs (the RNG is keyed by global pixel and sample).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,13 +45,15 @@ __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::valu
   trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterpN<VN>>(P);
 }
 
-// Per pixel: the f64 sum of each stratum row s_j (a row item's partial, or the sequential s_i
-// sum of a tail pair's per-sample values: the same running sum, bit for bit), then the rows in
-// s_j order (render.rs:185-189 adds every sample into one running sum; here the rows are summed
-// first, so the association differs from the reference only between rows). One wave per 8x8
-// tile, lane = pixel of the tile: each load instruction reads 64 * 8 contiguous bytes. Chunked
-// calls carry the running sum in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum),
-// bit2 overwrite.
+// Per pixel, in the reference's sample order (s_j, then s_i: render.rs:185-189): the f64 partial
+// of each block of kPoolSi samples (a segment item's running sum, or the sequential sum of a tail
+// block's per-sample values: the same running sum, bit for bit) added into one running total.
+// The reference adds every sample into that total; here a block's samples are summed first, so
+// the association differs from the reference's only between blocks. One wave per 8x8 tile,
+// lane = pixel of the tile: each load instruction reads 64 * 8 contiguous bytes. Chunked calls
+// carry the running total in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum), bit2
+// overwrite.
+constexpr int kRedU = 8;  // partials loaded ahead per step of rt_reduce
 __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part,
                                                  double* __restrict__ tot,
                                                  float* __restrict__ accum, int W, int n_rows,
@@ -67,30 +68,55 @@ __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part
   if (pv >= tile_w * tile_h) return;
   const int x = tx * kWaveTile + pv % tile_w, kr = ty * kWaveTile + pv / tile_w;
   const size_t i = (size_t)kr * W + x;
+  const int n_blk = (S + kPoolSi - 1) / kPoolSi;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   if (!(mode & 1)) {
     t0 = tot[3 * i];
     t1 = tot[3 * i + 1];
     t2 = tot[3 * i + 2];
   }
-  for (int k = 0; k < n_sj; ++k) {
-    const size_t q = (size_t)tile_id * n_sj + k;
-    double r0, r1, r2;
-    if (q < (size_t)n_pairs_a) {
-      const double* r = part + (q * 64 + pv) * 3;
-      r0 = r[0], r1 = r[1], r2 = r[2];
-    } else {
-      const double* r = part + ((size_t)n_pairs_a * 64 + (q - n_pairs_a) * (size_t)S * 64 + pv) * 3;
-      r0 = 0.0, r1 = 0.0, r2 = 0.0;
-#pragma unroll 4
-      for (int si = 0; si < S; ++si) {
-        const double* v = r + (size_t)si * 64 * 3;
-        r0 += v[0], r1 += v[1], r2 += v[2];
-      }
+  // segment pairs of this tile: their partials are consecutive (stride 64 values), s_j-major
+  const int k_a = max(0, min(n_sj, n_pairs_a - tile_id * n_sj));
+  const double* r = part + ((size_t)tile_id * n_sj * n_blk * 64 + pv) * 3;
+  const int M = k_a * n_blk;
+  int m = 0;
+  // loads first, then the in-order adds: 24 loads in flight per lane (a share's few waves are
+  // otherwise bound by one load's latency per partial)
+  for (; m + kRedU <= M; m += kRedU) {
+    double v[kRedU][3];
+#pragma unroll
+    for (int u = 0; u < kRedU; ++u) {
+      const double* e = r + (size_t)(m + u) * 192;
+      v[u][0] = e[0], v[u][1] = e[1], v[u][2] = e[2];
     }
-    t0 += r0;
-    t1 += r1;
-    t2 += r2;
+#pragma unroll
+    for (int u = 0; u < kRedU; ++u) t0 += v[u][0], t1 += v[u][1], t2 += v[u][2];
+  }
+  for (; m < M; ++m) {
+    const double* e = r + (size_t)m * 192;
+    t0 += e[0], t1 += e[1], t2 += e[2];
+  }
+  // tail pairs: per-sample values, summed per block of kPoolSi samples
+  for (int k = k_a; k < n_sj; ++k) {
+    const size_t q = (size_t)tile_id * n_sj + k;
+    const double* rt =
+        part + ((size_t)n_pairs_a * n_blk * 64 + (q - n_pairs_a) * (size_t)S * 64 + pv) * 3;
+    for (int s0 = 0; s0 < S; s0 += kPoolSi) {
+      const int n = min(kPoolSi, S - s0);
+      double v[kPoolSi][3];
+#pragma unroll
+      for (int u = 0; u < kPoolSi; ++u) {
+        if (u < n) {
+          const double* e = rt + (size_t)(s0 + u) * 192;
+          v[u][0] = e[0], v[u][1] = e[1], v[u][2] = e[2];
+        }
+      }
+      double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll
+      for (int u = 0; u < kPoolSi; ++u)
+        if (u < n) r0 += v[u][0], r1 += v[u][1], r2 += v[u][2];
+      t0 += r0, t1 += r1, t2 += r2;
+    }
   }
   float* a = accum + 3 * i;
   if (mode & 2) {
@@ -465,9 +491,6 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   const int tiles_y = (opts->n_rows + kWaveTile - 1) / kWaveTile;
   const int n_tiles = P.tiles_x * tiles_y;
   P.n_blk = (S + kPoolSi - 1) / kPoolSi;
-  P.regen_min = kRegenMin;
-  if (const char* e = std::getenv("RT_REGEN_MIN")) P.regen_min = std::atoi(e);  // A/B only
-  P.regen_min = std::max(1, std::min(64, P.regen_min));
   typedef void (*kern_t)(TraceParams);
   // [count][vol][tex][bvh]; a scene without a BVH whose tables are staged in LDS runs the
   // STAGED variant (LDS-typed table reads), BVH kernels read the tables from global memory
@@ -576,10 +599,11 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     sc->resident_lds[kslot] = lds_bytes;
   }
   const int64_t max_blocks = (int64_t)sc->resident_blocks[kslot] * std::max(1, sc->n_cu);
-  // Outputs (TraceParams::part): one f64 RGB partial per (pixel, s_j) of the row pairs and one
-  // per sample of the tail pairs. The tail is about one pair per resident wave (a pair is 64 x
-  // sqrt_spp paths): when the row pools run out, lanes still finishing a row have ~sqrt_spp / 2
-  // samples left, and the tail's single samples keep the other lanes busy meanwhile.
+  // Outputs (TraceParams::part): one f64 RGB partial per (pixel, s_j, block) of the segment
+  // pairs and one per sample of the tail pairs. The tail is about one pair per resident wave (a
+  // pair is 64 x sqrt_spp paths): when the segment pools run out, lanes still finishing a
+  // segment have ~kPoolSi / 2 samples left, and the tail's single samples keep the other lanes
+  // busy meanwhile.
   // RT_TAIL_PAIRS overrides it (tests: the image does not depend on the split).
   int64_t tail = max_blocks * (block / 64);
   if (const char* e = std::getenv("RT_TAIL_PAIRS")) tail = std::strtoll(e, nullptr, 10);
@@ -589,12 +613,11 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   size_t cap = (size_t)8192 << 20;
   if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
   const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
-  const size_t row_bytes = (size_t)64 * 3 * sizeof(double);  // one pair's row partials
-  const size_t tail_bytes = (size_t)S * row_bytes;           // one tail pair's samples
+  const size_t val_bytes = (size_t)64 * 3 * sizeof(double);  // one f64 RGB value per pixel
   auto part_bytes = [&](int cn) {
     const int64_t pairs = (int64_t)n_tiles * cn;
     const int64_t tb = std::min<int64_t>(pairs, tail);
-    return (size_t)(pairs - tb) * row_bytes + (size_t)tb * tail_bytes;
+    return ((size_t)(pairs - tb) * P.n_blk + (size_t)tb * S) * val_bytes;
   };
   int chunk = n_sj;
   while (chunk > 1 && tot_bytes + part_bytes(chunk) > cap) chunk = (chunk + 1) / 2;
@@ -627,7 +650,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
     P.sj0 = c0;
     P.n_sj = cn;
     P.n_pairs_a = (int)(pairs - tb);
-    P.n_pools = (int)(P.n_pairs_a + tb * P.n_blk);
+    P.n_pools = (int)(pairs * P.n_blk);
     // persistent grid: as many waves as the device holds at once (never more than pools)
     const int64_t blocks = std::min(max_blocks, ((int64_t)P.n_pools + (block / 64) - 1) / (block / 64));
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));

@@ -35,15 +35,15 @@ struct cond<false, T, F> {
 };
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 constexpr int kWaveTile = 8;  // 8x8 pixels per wave
-// Stratum columns s_i per pool: a pool is 8x8 pixels x one stratum row s_j x kPoolSi columns,
-// so the last pools of a launch leave at most ~kPoolSi paths per lane of tail (at 961 spp a
-// whole stratum row per pool left ~31: 9 % of an 8-GPU share of the C2 frame).
+// Stratum columns s_i per pool: a pool is 8x8 pixels x one stratum row s_j x kPoolSi columns.
+// A segment item (one pixel's kPoolSi consecutive samples in one lane) lasts ~kPoolSi paths, so
+// the launch drains within a few paths per lane (whole-row items, 31 paths at 961 spp, left an
+// 8-GPU share of the C2 frame 13 % idle at the end). A power of two.
 #ifndef RT_POOL_SI
 #define RT_POOL_SI 8
 #endif
 constexpr int kPoolSi = RT_POOL_SI;
-// Lanes that must wait before a wave generates their camera rays together (TraceParams::regen_min)
-constexpr int kRegenMin = 1;
+static_assert((kPoolSi & (kPoolSi - 1)) == 0, "kPoolSi: a power of two");
 constexpr int kBlock = 256;   // 4 waves per workgroup
 // BVH kernels run three waves per SIMD (MinWaves below: <= 168 VGPRs) in ONE 768-thread
 // workgroup per CU, so the workgroup may take (almost) the CU's whole 160 KiB LDS for the BVH
@@ -224,15 +224,16 @@ struct TraceParams {
   const uint32_t* __restrict__ lights;
   const uint32_t* __restrict__ light_offs;
   const uint8_t* __restrict__ texels;
-  // f64 RGB outputs of the launch (rt_reduce sums them): first the stratum-row partials of the
-  // row pairs [0, n_pairs_a) (index pair * 64 + pv), then the per-sample values of the tail
-  // pairs (index n_pairs_a * 64 + ((pair - n_pairs_a) * sqrt_spp + s_i) * 64 + pv)
+  // f64 RGB outputs of the launch (rt_reduce sums them): first the segment partials of the
+  // segment pairs [0, n_pairs_a) (index (pair * n_blk + blk) * 64 + pv), then the per-sample
+  // values of the tail pairs (index (n_pairs_a * n_blk + (pair - n_pairs_a) * sqrt_spp + s_i) *
+  // 64 + pv)
   double* __restrict__ part;
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  int n_pools;    // pools of this launch: n_pairs_a row pools, then (pairs - n_pairs_a) * n_blk
-  int n_pairs_a;  // (tile, s_j) pairs rendered as whole stratum rows per lane
-  int n_blk;      // s_i blocks per tail pair: ceil(sqrt_spp / kPoolSi)
+  int n_pools;    // pools of this launch: pairs * n_blk, pool id = pair * n_blk + blk
+  int n_pairs_a;  // (tile, s_j) pairs rendered as segment items (the rest: one item per sample)
+  int n_blk;      // s_i blocks (segments) per pair: ceil(sqrt_spp / kPoolSi)
   uint32_t root, n_lights, lights_is_list, flags;
   uint32_t lights_nested;  // some light entry is a nested HittableList (RTL_LLIST)
   int sphere_light0;    // index of the first SPHERE light record, -1 if none
@@ -255,7 +256,6 @@ struct TraceParams {
   int W, n_rows, row_begin, row_step, sqrt_spp, sj0, n_sj, max_depth;
   uint32_t seed_lo, seed_hi;
   int tiles_x;
-  int regen_min;  // camera rays of waiting lanes are generated once this many lanes wait (§4.1)
 };
 
 // The kernel's only argument sits at offset 0 of the kernarg segment. Camera constants are read
@@ -1582,15 +1582,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   do {          \
   } while (0)
 #endif
-  // Persistent waves over a global pool queue. A pool is a (tile, s_j) pair of
-  // one 8x8 pixel tile and one stratum row s_j, or a block of kPoolSi stratum columns of one:
-  //  * row pools (pairs [0, n_pairs_a)): one item per pixel = the whole stratum row (pixel, s_j);
-  //    the lane traces its sqrt_spp samples in the reference's s_i order (render.rs:185-189) and
-  //    keeps their f64 running sum in LDS, then writes ONE f64 RGB partial per (pixel, s_j);
-  //  * tail pools (the last pairs, per s_i block): one item per pixel-sample, written as f64 RGB
-  //    to its own output value; rt_reduce sums a tail pair's samples in s_i order, which is the
-  //    running sum a row item computes, bit for bit. The tail keeps lanes busy while the last
-  //    rows finish, so the launch ends within a few paths per lane.
+  // Persistent waves over a global pool queue. A pool is one 8x8 pixel tile x
+  // one stratum row s_j x one block of kPoolSi stratum columns s_i:
+  //  * segment pools (pairs [0, n_pairs_a)): one item per pixel = the block's samples of the
+  //    pixel; the lane traces them in the reference's s_i order (render.rs:185-189), keeps their
+  //    f64 running sum in LDS, then writes ONE f64 RGB partial per (pixel, s_j, block);
+  //  * tail pools (the last pairs): one item per pixel-sample, written as f64 RGB to its own
+  //    output value; rt_reduce sums a tail block's samples in s_i order, which is the running
+  //    sum a segment item computes, bit for bit. The tail keeps lanes busy while the last
+  //    segments finish, so the launch ends within a path or two per lane.
   // Idle lanes claim the next item of the wave's pool (ballot + mbcnt), across pool boundaries,
   // so lanes only idle at the very end of the launch. Wave-uniform pool state:
   const int lane = threadIdx.x & 63;
@@ -1600,7 +1600,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   const bool have_lights = P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
   constexpr int NB = BlockOf<BVH>::value;
-  // per-lane f64 running sum of the item in flight (row items: the stratum row so far)
+  // per-lane f64 running sum of the item in flight (segment items: the block's samples so far)
   __shared__ double sh_acc[3 * NB];
   const int tid = threadIdx.x;
 
@@ -1614,27 +1614,31 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   uint32_t sij = 0;    // s_j << 16 | s_i of the sample in flight
   int next = 0;        // pool items claimed so far (wave-uniform)
   Rng g = {0u, 0u, 0u, 0u};
-  // A sample's radiance is final: add it to the item's running sum; a row item continues with
-  // its next s_i, a finished item writes its f64 sum.
+  // A sample's radiance is final: add it to the item's running sum; a segment item continues
+  // with its next s_i, a finished item writes its f64 sum.
   auto end_sample = [&](d3 L) {
+    // launch constants through the opaque kernarg pointer: read at the point of use instead of
+    // being held in SGPRs across the path loop (kparams())
+    const kparams_t Q = kparams();
     L = xs_resolve(L, (uint32_t)depth >> 24);
     double a0 = sh_acc[tid] + L.x, a1 = sh_acc[NB + tid] + L.y, a2 = sh_acc[2 * NB + tid] + L.z;
     alive = false;
-    if (!(xk >> 31) && (int)(sij & 0xffffu) + 1 < P.sqrt_spp) {
+    const int s_n = (int)(sij & 0xffffu) + 1;
+    if (!(xk >> 31) && (s_n & (kPoolSi - 1)) != 0 && s_n < Q->sqrt_spp) {
       sh_acc[tid] = a0, sh_acc[NB + tid] = a1, sh_acc[2 * NB + tid] = a2;
       sij += 1u;
       fresh = true;
     } else {  // the item's output index (TraceParams::part), from its pixel and stratum
       const int x = (int)(xk & 0xffffu), kr = (int)((xk >> 16) & 0x7fffu);
-      const int tx = x >> 3, tw = imin(kWaveTile, P.W - tx * kWaveTile);
+      const int tx = x >> 3, tw = imin(kWaveTile, Q->W - tx * kWaveTile);
       const uint32_t pv = (uint32_t)((kr & 7) * tw + (x & 7));
-      const uint32_t qq = (uint32_t)((kr >> 3) * P.tiles_x + tx) * (uint32_t)P.n_sj +
-                          ((sij >> 16) - (uint32_t)P.sj0);
+      const uint32_t qq = (uint32_t)((kr >> 3) * Q->tiles_x + tx) * (uint32_t)Q->n_sj +
+                          ((sij >> 16) - (uint32_t)Q->sj0);
+      const uint32_t nb = (uint32_t)Q->n_blk, na = (uint32_t)Q->n_pairs_a;
       const uint32_t outi =
-          (xk >> 31) ? ((uint32_t)P.n_pairs_a + (qq - (uint32_t)P.n_pairs_a) * (uint32_t)P.sqrt_spp +
-                        (sij & 0xffffu)) * 64u + pv
-                     : qq * 64u + pv;
-      double* o = P.part + (size_t)outi * 3;
+          (xk >> 31) ? (na * nb + (qq - na) * (uint32_t)Q->sqrt_spp + (sij & 0xffffu)) * 64u + pv
+                     : (qq * nb + (sij & 0xffffu) / (uint32_t)kPoolSi) * 64u + pv;
+      double* o = Q->part + (size_t)outi * 3;
       o[0] = a0, o[1] = a1, o[2] = a2;
     }
   };
@@ -1646,28 +1650,22 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     const bool idle = !alive && !fresh;
     const unsigned long long want = __ballot(idle);
     if (want != 0ull && next >= pool && more) {  // current pool drained: take the next one
+      const kparams_t Q = kparams();
       uint32_t id = 0u;
-      if (lane == 0) id = atomicAdd(P.queue, 1u);
+      if (lane == 0) id = atomicAdd(Q->queue, 1u);
       id = __builtin_amdgcn_readfirstlane(id);
-      if ((int)id < P.n_pools) {
-        int blk = 0;
-        tailp = (int)id >= P.n_pairs_a;
-        if (tailp) {
-          const int b = (int)id - P.n_pairs_a;
-          const int qb = b / P.n_blk;
-          blk = b - qb * P.n_blk;
-          q = P.n_pairs_a + qb;
-        } else {
-          q = (int)id;
-        }
-        const int tile = q / P.n_sj;
-        tx = tile % P.tiles_x;
-        ty = tile / P.tiles_x;
-        tile_w = imin(kWaveTile, P.W - tx * kWaveTile);
-        nv = tile_w * imin(kWaveTile, P.n_rows - ty * kWaveTile);
+      if ((int)id < Q->n_pools) {
+        q = (int)id / Q->n_blk;
+        const int blk = (int)id - q * Q->n_blk;
+        tailp = q >= Q->n_pairs_a;
+        const int tile = q / Q->n_sj;
+        tx = tile % Q->tiles_x;
+        ty = tile / Q->tiles_x;
+        tile_w = imin(kWaveTile, Q->W - tx * kWaveTile);
+        nv = tile_w * imin(kWaveTile, Q->n_rows - ty * kWaveTile);
         si0 = blk * kPoolSi;
-        pool = tailp ? nv * imin(kPoolSi, P.sqrt_spp - si0) : nv;
-        s_jp = P.sj0 + (q - tile * P.n_sj);
+        pool = tailp ? nv * imin(kPoolSi, Q->sqrt_spp - si0) : nv;
+        s_jp = Q->sj0 + (q - tile * Q->n_sj);
       } else {
         more = false;
         pool = 0;
@@ -1687,7 +1685,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
           pv = k % nv;
           s_i = si0 + k / nv;
         }
-        if (!tailp) s_i = 0;
+        if (!tailp) s_i = si0;
         const int x = tx * kWaveTile + pv % tile_w;
         const int kr = ty * kWaveTile + pv / tile_w;
         xk = (uint32_t)x | (uint32_t)kr << 16 | (tailp ? 0x80000000u : 0u);
@@ -1697,11 +1695,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       }
     }
     next += __popcll(want);
-    // Camera rays for the lanes waiting on one (claimed items, next s_i) are generated together
-    // once regen_min lanes wait, or when no path is in flight: the block then runs at a higher
-    // lane utilisation. A sample's arithmetic does not depend on when it starts.
-    const unsigned long long wf = __ballot(fresh);
-    if (wf != 0ull && (__popcll(wf) >= P.regen_min || __ballot(alive) == 0ull) && fresh) {
+    if (fresh) {
       const kparams_t Q = kparams();
       const int x = (int)(xk & 0xffffu);
       const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
@@ -1731,7 +1725,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       tm = rnd(g);
       beta = mk(1., 1., 1.);
       Lp = mk(0., 0., 0.);
-      depth = P.max_depth;  // RT_XS_* cleared
+      depth = Q->max_depth;  // RT_XS_* cleared
       alive = true;
       fresh = false;
     }

@@ -28,7 +28,13 @@ for spec in filter(None, os.environ.get("AB_ENVS", "").split(";")):
 blob, cam = rt.preset_blob(SCENE, width=W, spp=SPP)
 libs, scenes = [], []
 for p in paths:
-    lib = rt.load_device_lib(p.split("[")[0]) if "[" not in p else libs[0]
+    if "[" in p:
+        lib = libs[0]
+    else:
+        try:
+            lib = rt.load_device_lib(p)
+        except AttributeError:  # an older ABI (e.g. a previous round's library): plain ctypes
+            lib = C.CDLL(p)
     h = C.c_void_p()
     assert lib.rt_scene_create(blob.ref(), 0, C.byref(h)) == 0, lib.rt_last_error()
     libs.append(lib)
