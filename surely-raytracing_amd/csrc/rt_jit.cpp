@@ -515,6 +515,15 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   std::vector<const char*> opts = {off.c_str(), "-O3", "-std=c++17", "-ffp-contract=off",
                                    "-fno-gpu-flush-denormals-to-zero", "-mllvm",
                                    "-amdgpu-spill-vgpr-to-agpr=0"};
+#ifndef RT_JIT_MLICM
+  // No machine-level loop-invariant hoisting: it lifts the f64 literal constants of the math
+  // inside the path loop (the log of ConstantMedium, sphere_uv's acos/atan2, polynomial
+  // coefficients) out of the loop into VGPR pairs that stay live across every bounce, and the
+  // register allocator then spills them rather than rematerialise them (final_scene: 168 VGPRs
+  // + 24 spilled, cornell_smoke 128 + 10; without: 148 + 0 and 117 + 0). DESIGN.md §4.1b.
+  opts.push_back("-mllvm");
+  opts.push_back("-disable-machine-licm");
+#endif
   // build knobs of this library (ablation / occupancy variants, Makefile) apply to its
   // run-time kernels too
 #define RTJ_STR2(x) #x
@@ -548,6 +557,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #endif
 #ifdef RT_ABL_TWICE_BVH
   opts.push_back("-DRT_ABL_TWICE_BVH=" RTJ_STR(RT_ABL_TWICE_BVH));
+#endif
+#ifdef RT_NO_PK_BOX
+  opts.push_back("-DRT_NO_PK_BOX");
 #endif
 #ifdef RT_ABL_NOXS
   opts.push_back("-DRT_ABL_NOXS");

@@ -167,6 +167,19 @@ __device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-2
   return vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), n, perp);
 }
 
+// An f64 constant materialised at its point of use: two s_mov_b32 into an SGPR pair, which the
+// fma reads directly. The compiler otherwise hoists literal constants out of the path loop into
+// VGPR pairs and, short of registers, spills them (final_scene: 12 of the 24 spilled VGPRs were
+// sincos2pi's coefficients); volatile asm is not hoisted.
+template <uint64_t B>
+__device__ __forceinline__ double kd_bits() {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)B));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(B >> 32)));
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+#define KD(x) kd_bits<__builtin_bit_cast(uint64_t, (double)(x))>()
+
 // sin(2*pi*u), cos(2*pi*u) for u in [0, 1) (vec3.rs:244, object.rs:127: phi = 2*pi*r1).
 // Exact reduction to a quarter-turn fraction r in [-1/2, 1/2], then Taylor series of
 // theta = r*pi/2 (|theta| <= pi/4) to theta^19 / theta^18: < 1 ulp, and none of the large-
@@ -176,24 +189,24 @@ __device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
   double k = floor(t + 0.5);
   double th = (t - k) * (0.5 * kPi);
   double x2 = th * th;
-  double s = 1.0 / 121645100408832000.0;  // 1/19!
-  s = s * -x2 + 1.0 / 355687428096000.0;
-  s = s * -x2 + 1.0 / 1307674368000.0;
-  s = s * -x2 + 1.0 / 6227020800.0;
-  s = s * -x2 + 1.0 / 39916800.0;
-  s = s * -x2 + 1.0 / 362880.0;
-  s = s * -x2 + 1.0 / 5040.0;
-  s = s * -x2 + 1.0 / 120.0;
-  s = s * -x2 + 1.0 / 6.0;
+  double s = KD(1.0 / 121645100408832000.0);  // 1/19!
+  s = s * -x2 + KD(1.0 / 355687428096000.0);
+  s = s * -x2 + KD(1.0 / 1307674368000.0);
+  s = s * -x2 + KD(1.0 / 6227020800.0);
+  s = s * -x2 + KD(1.0 / 39916800.0);
+  s = s * -x2 + KD(1.0 / 362880.0);
+  s = s * -x2 + KD(1.0 / 5040.0);
+  s = s * -x2 + KD(1.0 / 120.0);
+  s = s * -x2 + KD(1.0 / 6.0);
   s = (s * -x2 + 1.0) * th;
-  double c = 1.0 / 6402373705728000.0;  // 1/18!
-  c = c * -x2 + 1.0 / 20922789888000.0;
-  c = c * -x2 + 1.0 / 87178291200.0;
-  c = c * -x2 + 1.0 / 479001600.0;
-  c = c * -x2 + 1.0 / 3628800.0;
-  c = c * -x2 + 1.0 / 40320.0;
-  c = c * -x2 + 1.0 / 720.0;
-  c = c * -x2 + 1.0 / 24.0;
+  double c = KD(1.0 / 6402373705728000.0);  // 1/18!
+  c = c * -x2 + KD(1.0 / 20922789888000.0);
+  c = c * -x2 + KD(1.0 / 87178291200.0);
+  c = c * -x2 + KD(1.0 / 479001600.0);
+  c = c * -x2 + KD(1.0 / 3628800.0);
+  c = c * -x2 + KD(1.0 / 40320.0);
+  c = c * -x2 + KD(1.0 / 720.0);
+  c = c * -x2 + KD(1.0 / 24.0);
   c = c * -x2 + 0.5;
   c = c * -x2 + 1.0;
   int q = ((int)k) & 3;
@@ -1031,6 +1044,7 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
 // the slab test keeps every box whose entry is <= closest * (1 + kTieRel), so no candidate the
 // flag logic must see is culled.
 constexpr double kTieRel = 0x1p-30;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool MAIN>
 __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double tm, int frame,
                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
@@ -1051,6 +1065,10 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
   constexpr float kBoxRel = 0x1p-20f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
+#ifndef RT_NO_PK_BOX
+  const f32x2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
+  const f32x2 ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
+#endif
   const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
   double closest = tmax;
   float close_f = (float)(closest + closest * (2.0 * kTieRel));
@@ -1080,9 +1098,19 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
     while (e < hd.x) {
       s = S[2 * e];
       const uint4 s2 = S[2 * e + 1];
+#ifndef RT_NO_PK_BOX
+      // (near, far) bound pairs: one packed f32 subtract and multiply per axis (v_pk_add_f32,
+      // v_pk_mul_f32), the same two roundings per slab time as the scalar form
+      const f32x2 bx = {__uint_as_float(s.z), __uint_as_float(s.w)};
+      const f32x2 by = {__uint_as_float(s2.x), __uint_as_float(s2.y)};
+      const f32x2 bz = {__uint_as_float(s2.z), __uint_as_float(s2.w)};
+      const f32x2 tx2 = (bx - ox2) * ix2, ty2 = (by - oy2) * iy2, tz2 = (bz - oz2) * iz2;
+      const float tnx = tx2.x, tfx = tx2.y, tny = ty2.x, tfy = ty2.y, tnz = tz2.x, tfz = tz2.y;
+#else
       const float tnx = (__uint_as_float(s.z) - ox) * ix, tfx = (__uint_as_float(s.w) - ox) * ix;
       const float tny = (__uint_as_float(s2.x) - oy) * iy, tfy = (__uint_as_float(s2.y) - oy) * iy;
       const float tnz = (__uint_as_float(s2.z) - oz) * iz, tfz = (__uint_as_float(s2.w) - oz) * iz;
+#endif
       // fmaxf / fminf drop a NaN bound (o on the bound's plane with inv = +-inf): no constraint
       const float tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
       const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
@@ -1327,12 +1355,20 @@ __device__ d3 tex_value(const TraceParams& P, const TT& T, uint32_t id, double u
   return mk(0., 0., 0.);
 }
 
-// get_sphere_uv object.rs:114-120 (out of line: only image-textured spheres need it)
-__device__ __noinline__ void sphere_uv(d3 p, double& u, double& v) {
+// get_sphere_uv object.rs:114-120 (out of line: only image-textured spheres need it; (u, v)
+// come back in registers, not through a stack slot)
+struct UV {
+  double u, v;
+};
+__device__ __noinline__ UV sphere_uv_f(d3 p) {
   double theta = acos(-p.y);
   double phi = atan2(-p.z, p.x) + kPi;
-  u = phi * (1.0 / kPi) * 0.5;
-  v = theta * (1.0 / kPi);
+  return {phi * (1.0 / kPi) * 0.5, theta * (1.0 / kPi)};
+}
+__device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {
+  const UV r = sphere_uv_f(p);
+  u = r.u;
+  v = r.v;
 }
 
 // ---------------------------------------------------------------- sampling
