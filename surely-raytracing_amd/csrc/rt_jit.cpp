@@ -447,6 +447,45 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
        "    hf = hit ? fr : hf;\n"
        "    return hit;\n"
        "  }\n";
+  // The hit record's frame (rt_kernel.h TravInterpN::frame_in / frame_out): every frame the walk
+  // can report, its chain unrolled with literals (the same translate/rotate arithmetic as
+  // xform_in / xform_out); frames inside BVH subtrees take the interpreter's chain walk.
+  std::ostringstream fi, fo;
+  for (size_t id = 1; id < G.frames.size(); ++id) {
+    const size_t f = (size_t)G.frames[id];
+    const uint32_t len = N[f + 2];
+    const bool lng = (N[f] & RTL_XFORM_LONG) != 0u;
+    std::vector<size_t> chain;
+    for (uint32_t k = 0; k < len; ++k) chain.push_back(lng ? N[(size_t)N[f + 4] + k] : N[f + 4 + k]);
+    fi << "    " << (id > 1 ? "} else if" : "if") << " (hf == " << f << ") {\n";
+    fo << "    " << (id > 1 ? "} else if" : "if") << " (hf == " << f << ") {\n";
+    for (size_t x : chain) {
+      if ((N[x] & 0xffu) == RTL_TRANSLATE)
+        fi << "      translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4)) << ", o);\n";
+      else
+        fi << "      rotate_y_in(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3)) << ", o, d);\n";
+    }
+    for (size_t k = chain.size(); k-- > 0;) {
+      const size_t x = chain[k];
+      if ((N[x] & 0xffu) == RTL_TRANSLATE)
+        fo << "      translate_out(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4)) << ", p);\n";
+      else
+        fo << "      rotate_y_out(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3)) << ", p, n);\n";
+    }
+  }
+  // without BVH subtrees the frames above are all the walk can report
+  const bool many = G.frames.size() > 1;
+  const std::string more = G.bvh ? (many ? "    } else if (hf >= 0) {\n" : "    if (hf >= 0) {\n") : "";
+  const std::string rest_in = G.bvh ? "      frame_ray(Nd, hf, wo, wd, o, d);\n    }\n" : (many ? "    }\n" : "");
+  const std::string rest_out = G.bvh ? "      rtk::frame_out(Nd, hf, p, n);\n    }\n" : (many ? "    }\n" : "");
+  o << "  template <class TP>\n"
+       "  static __device__ __forceinline__ void frame_in(TP Nd, int hf, d3 wo, d3 wd, d3& o, d3& d) {\n"
+       "    (void)Nd;\n    o = wo;\n    d = wd;\n"
+    << fi.str() << more << rest_in << "  }\n"
+    << "  template <class TP>\n"
+       "  static __device__ __forceinline__ void frame_out(TP Nd, int hf, d3& p, d3& n) {\n"
+       "    (void)Nd; (void)hf; (void)p; (void)n;\n"
+    << fo.str() << more << rest_out << "  }\n";
   if (!gen_lights_pdf(F, o, why)) return "";
   o << "};\n";
   return pre.str() + o.str();

@@ -576,6 +576,12 @@ __device__ __forceinline__ void xform_out(Ptr X, d3& p, d3& n) {
     n = mk(fma(c, n.x, s * n.z), n.y, fma(-s, n.x, c * n.z));
   }
 }
+// xform_out on constants already in registers (generated frame code, rt_jit.cpp)
+__device__ __forceinline__ void translate_out(d3 off, d3& p) { p = p + off; }
+__device__ __forceinline__ void rotate_y_out(double s, double c, d3& p, d3& n) {
+  p = mk(fma(c, p.x, s * p.z), p.y, fma(-s, p.x, c * p.z));
+  n = mk(fma(c, n.x, s * n.z), n.y, fma(-s, n.x, c * n.z));
+}
 // Local ray of `frame` = the world ray pushed through its transform chain, root first.
 template <class Ptr>
 __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o, d3& d) {
@@ -592,6 +598,21 @@ __device__ __forceinline__ void frame_ray(Ptr N, int frame, d3 wo, d3 wd, d3& o,
 #pragma unroll
   for (int k = 0; k < RTL_MAX_CHAIN; ++k)
     if ((uint32_t)k < h.z) xform_in(N + c4[k], o, d);
+}
+// A hit point and normal of `frame` back to world space, innermost transform first.
+template <class Ptr>
+__device__ __forceinline__ void frame_out(Ptr N, int frame, d3& p, d3& n) {
+  if (frame < 0) return;
+  const uint4 fh = ld4u(N + frame);
+  const uint4 ch = ld4u(N + frame + 4);
+  if (fh.x & RTL_XFORM_LONG) {
+    for (uint32_t k = fh.z; k-- > 0;) xform_out(N + N[ch.x + k], p, n);
+    return;
+  }
+  const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+  for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
+    if ((uint32_t)k < fh.z) xform_out(N + c4[k], p, n);
 }
 
 // ConstantMedium::hit's two boundary queries (constant_medium.rs:46-55) in ONE wave-uniform walk
@@ -1547,6 +1568,16 @@ struct TravInterpN {
                                                       double cos_sl0, Ctr<COUNT>& C) {
     return light_pdf<COUNT>(P, origin, dir, cos_sl0, C);
   }
+  // the hit record's frame (transform.rs:57-135): the world ray into the winner's frame, and its
+  // hit point / normal back out
+  template <class TP>
+  static __device__ __forceinline__ void frame_in(TP N, int hf, d3 wo, d3 wd, d3& o, d3& d) {
+    frame_ray(N, hf, wo, wd, o, d);
+  }
+  template <class TP>
+  static __device__ __forceinline__ void frame_out(TP N, int hf, d3& p, d3& n) {
+    rtk::frame_out(N, hf, p, n);
+  }
 };
 typedef TravInterpN<0> TravInterp;
 
@@ -1649,7 +1680,9 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   uint32_t xk = 0;     // x | row-in-call << 16 | tail item << 31
   uint32_t sij = 0;    // s_j << 16 | s_i of the sample in flight
   int next = 0;        // pool items claimed so far (wave-uniform)
-  Rng g = {0u, 0u, 0u, 0u};
+  // a valid (non-zero) xoshiro state from the start: lanes without a path still run bounces on
+  // stale rays at the end of a launch, and the rejection loops (random_unit_vector) must end
+  Rng g = {0x9E3779B9u, 1u, 2u, 3u};
   // A sample's radiance is final: add it to the item's running sum; a segment item continues
   // with its next s_i, a finished item writes its f64 sum.
   auto end_sample = [&](d3 L) {
@@ -1764,21 +1797,31 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       depth = Q->max_depth;  // RT_XS_* cleared
       alive = true;
       fresh = false;
+      if (Q->max_depth == 0) {  // uniform: ray_color's depth guard (render.rs:260-262) at once
+        C.inc(RT_OP_DEPTH_CUTOFF);
+        end_sample(mk(0., 0., 0.));
+      }
     }
-    if (__ballot(alive) == 0ull) {
-      if (!more) break;
-      continue;
-    }
-    if (!alive) continue;
-    // One bounce. `break` leaves the block: the path bounced (metal) or ended (term: depth
-    // cut-off, miss, light); the ending lanes of all three kinds then share ONE end_sample.
+    // one back edge only (a `continue` here would give the loop header a second incoming state
+    // and the compiler a full copy of it); a wave with no path in flight but more pools to
+    // claim (a pool boundary) runs one bounce on stale rays, which the lanes then drop
+    if (!more && __ballot(alive) == 0ull) break;
+    // One bounce, run by EVERY lane of the wave (product kernels): a lane without a path (only
+    // at the very end of a launch) traces its stale ray and its result is dropped below. The
+    // scattered ray and throughput factor are committed unconditionally after the block, and
+    // the lanes that ended (miss, light) leave them undefined: the path state then has no value
+    // that survives the block on some lanes only, which would make the compiler copy the whole
+    // state (24 VGPRs) into join registers on every bounce. `break` leaves the block; the ending
+    // lanes then share ONE end_sample. ray_color's depth guard (render.rs:260-262) is applied
+    // where the depth is decremented (a fresh path starts with max_depth >= 1; at max_depth 0
+    // the camera-ray block ends every sample at once).
     bool term = false;
-    do {
-    if ((depth & 0xffffff) == 0) {  // ray_color depth guard render.rs:260-262
-      C.inc(RT_OP_DEPTH_CUTOFF);
-      term = true;
-      break;
-    }
+    d3 p_next, d_next, f_next;  // the scattered ray and this bounce's throughput factor
+    const bool run = COUNT ? alive : true;
+    if (!run) {
+      term = alive;
+      C.inc_if(RT_OP_DEPTH_CUTOFF, alive);
+    } else do {
     C.inc(RT_OP_WORLD_QUERIES);
     PROF(1);
 #ifdef RT_PROF
@@ -1813,7 +1856,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     const TP X = T.nodes + hn;
     uint32_t type = X[0] & 0xffu;
     d3 o, d;
-    frame_ray(T.nodes, hf, ro, rd, o, d);
+    Trav::frame_in(T.nodes, hf, ro, rd, o, d);
 #ifdef RT_ABL_HIT2  // ablation build: the hit record's frame recomputed (transform chain) twice
     {
       d3 o2, d2, ro2 = ro;
@@ -1849,18 +1892,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     } else {  // volume (constant_medium.rs:82-90)
       normal = mk(1., 0., 0.);
     }
-    if (hf >= 0) {  // back to world space, innermost transform first
-      uint4 fh = ld4u(T.nodes + hf);
-      uint4 ch = ld4u(T.nodes + hf + 4);
-      if (fh.x & RTL_XFORM_LONG) {
-        for (uint32_t k = fh.z; k-- > 0;) xform_out(T.nodes + T.nodes[ch.x + k], p, normal);
-      } else {
-        const uint32_t c4[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-        for (int k = RTL_MAX_CHAIN - 1; k >= 0; --k)
-          if ((uint32_t)k < fh.z) xform_out(T.nodes + c4[k], p, normal);
-      }
-    }
+    Trav::frame_out(T.nodes, hf, p, normal);  // back to world space
     const uint32_t kind = mh.x & 0xffu;
     PROF(3);
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
@@ -1873,11 +1905,9 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       C.inc(RT_OP_METAL);
       d3 reflected = reflect(unit_vector(rd), normal);
       d3 ruv = random_unit_vector(g);
-      reflected = vfma(ldd(M, 3), ruv, unit_vector(reflected));
-      beta = beta * ld3(M, 0);
-      ro = p;
-      rd = reflected;
-      --depth;
+      p_next = p;
+      d_next = vfma(ldd(M, 3), ruv, unit_vector(reflected));
+      f_next = ld3(M, 0);
       break;
     }
     // Dielectric (material.rs:166-191), Lambertian and Isotropic (the mixture-PDF branch,
@@ -2023,12 +2053,20 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       dir = refl ? reflect(uu, normal) : refr;
       factor = ld3(M, 0);  // attenuation = tint
     }
-    beta = beta * factor;
-    ro = p;
-    rd = dir;
-    --depth;
+    p_next = p;
+    d_next = dir;
+    f_next = factor;
     } while (false);
-    if (term) end_sample(Lp);
+    if (run) {  // wave-uniform: commit the bounce (garbage on ending lanes, never read)
+      ro = p_next;
+      rd = d_next;
+      beta = beta * f_next;
+      --depth;  // ending lanes had depth >= 1: the RT_XS_* bits above it are untouched
+      const bool cut = !term && (depth & 0xffffff) == 0;
+      C.inc_if(RT_OP_DEPTH_CUTOFF, cut);
+      term |= cut;
+    }
+    if (term & alive) end_sample(Lp);
   }
 #ifdef RT_PROF
   PROF(7);

@@ -47,7 +47,7 @@ def test_cornell_walker_sequence():
     blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
     state, src = rt.jit_check(blob)
     assert state == 1
-    world = src[:src.index("lights_pdf")]
+    world = src[:src.index("void frame_in")]
     calls = re.findall(r"(aquad_test<COUNT, \d>|quad_test<COUNT>|sphere_test_v<COUNT>|translate_in|"
                        r"rotate_y_in|o = ro;)", world)
     assert calls[:6] == ["aquad_test<COUNT, 0>"] * 2 + ["aquad_test<COUNT, 1>"] * 3 + ["aquad_test<COUNT, 2>"]
@@ -59,6 +59,14 @@ def test_cornell_walker_sequence():
     assert all(struct.pack("<d", v) == struct.pack("<d", float.fromhex(v.hex())) for v in lits)
     # rcp of each axis formed once per frame: 3 in the world frame, 3 in the box frame
     assert len(re.findall(r"r[xyz] = rcp_nr1", world)) == 6
+    # the hit record's frame (transform.rs:57-135) for the box: the same chain with the same
+    # literals, into the frame root first and back out innermost first; no interpreter fallback
+    fin = src[src.index("void frame_in"):src.index("void frame_out")]
+    fout = src[src.index("void frame_out"):src.index("lights_pdf")]
+    box = "(0x1.09p+8), (0x0p+0), (0x1.27p+8)"
+    assert "hf == 308" in fin and fin.index("translate_in(mk(" + box) < fin.index("rotate_y_in(")
+    assert "hf == 308" in fout and fout.index("rotate_y_out(") < fout.index("translate_out(mk(" + box)
+    assert "frame_ray" not in fin and "rtk::frame_out" not in fout
 
 
 def test_cornell_lights_pdf_unrolled():

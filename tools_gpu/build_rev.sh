@@ -1,12 +1,11 @@
 #!/bin/bash
-# Build the device library of git revision $1 into build/variants/librtmi355x_$2.so (A/B baseline)
+# Build the device library of git revision $1 into build/variants/librtmi355x_$2.so (A/B baseline
+# for tools_gpu/ab_variants.py), with the revision's own Makefile.
 set -e
 REV=${1:-HEAD}; NAME=${2:-prev}
 TMP=$(mktemp -d)
-git archive "$REV" surely-raytracing_amd/csrc include | tar -x -C "$TMP"
+git archive "$REV" Makefile include surely-raytracing_amd/csrc | tar -x -C "$TMP"
+make -C "$TMP" device > "$TMP/make.log" 2>&1 || { tail -20 "$TMP/make.log"; exit 1; }
 mkdir -p build/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-function \
-  -I"$TMP/include" -I"$TMP/surely-raytracing_amd/csrc" -shared \
-  "$TMP/surely-raytracing_amd/csrc/rt_device.hip" "$TMP/surely-raytracing_amd/csrc/rt_flatten.cpp" \
-  -o "build/variants/librtmi355x_$NAME.so"
+cp "$TMP/build/librtmi355x.so" "build/variants/librtmi355x_$NAME.so"
 rm -rf "$TMP"
