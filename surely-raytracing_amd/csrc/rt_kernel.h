@@ -226,6 +226,37 @@ __device__ __forceinline__ void sincos2pi(double u, double* so, double* co) {
   *co = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, sw ? s : c) ^ mc);
 }
 
+// log(x) of a uniform draw x = k * 2^-32, k in [0, 2^32) (random_double, utils.rs:5-7), for
+// ConstantMedium's free-flight distance (constant_medium.rs:75). fdlibm's reduction: x = 2^e m,
+// m in [sqrt(1/2), sqrt(2)), f = m - 1, s = f / (2 + f), log(m) = f - hfsq + s (hfsq + R(s^2)),
+// with R a near-minimax polynomial of degree 7 fitted in 200-bit arithmetic (tools_gpu/
+// fit_log.py: 0.77 ulp worst case over the draws, like the libm result within an ulp) and ln 2
+// split so that e * ln2_hi is exact. About 30 f64 operations against the 95 of the general
+// double-double library log; log(0) = -inf as in the reference (hit distance +inf: no scatter).
+__device__ __forceinline__ double log_u01(double x) {
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  int e = __builtin_amdgcn_frexp_exp(x);
+  const bool low = m < 0x1.6a09e667f3bcdp-1;  // sqrt(1/2)
+  m = low ? m * 2.0 : m;
+  e = low ? e - 1 : e;
+  const double f = m - 1.0;
+  const double hfsq = 0.5 * f * f;
+  const double s = div_nr(f, 2.0 + f);
+  const double z = s * s;
+  double r = 0x1.2b5726b357134p-3;
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.39fe7a28d6e94p-3)>(r, z);
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.7462b3d0fabd6p-3)>(r, z);
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.c71c62e8d3992p-3)>(r, z);
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.2492492dee5a0p-2)>(r, z);
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.9999999995300p-2)>(r, z);
+  r = fma_k<__builtin_bit_cast(uint64_t, 0x1.5555555555558p-1)>(r, z);
+  const double R = r * z;
+  const double dk = (double)e;
+  const double t = fma(s, hfsq + R, dk * 0x1.be8e7bcd5e4f2p-27);  // ln2_lo
+  const double v = dk * 0x1.62e42f8000000p-1 - ((hfsq - t) - f);  // ln2_hi
+  return x == 0.0 ? -kInf : v;
+}
+
 // Perlin tables staged per workgroup (dynamic LDS of the TEX kernels: n_perlin_lds tables)
 constexpr uint32_t kPerlinLds = 4;
 // Scenes whose node/material/texture/light tables (+ Perlin tables) fit this many bytes are
@@ -829,7 +860,7 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
       double ray_length = sqrt_nr(dot(d, d));
       double dist_inside = (t2 - t1) * ray_length;
       C.inc(RT_OP_VOLUME_DRAWS);
-      double hit_distance = ldd(X, 0) * log(rnd(g));
+      double hit_distance = ldd(X, 0) * log_u01(rnd(g));
       if (!(hit_distance > dist_inside)) {
         t_hit = t1 + div_nr(hit_distance, ray_length);
         return true;
