@@ -206,8 +206,9 @@ int rt_scene_validate(const rt_scene_blob* blob);
 /* Host-only diagnostics of the flattened layout (no device needed): out[0..8] = node words,
  * BVH-region words, BVH records, DUP records (span-1 leaves tested once), ConstantMedium
  * records, of which one-walk sphere / one-walk quad boundaries, light records, and BVH
- * subtrees walked through an ordered BVH by the product kernels. */
-#define RT_LAYOUT_STATS 9
+ * subtrees walked through an ordered BVH by the product kernels, of those the ones with a compact
+ * copy for the walk from LDS, and the bytes of that compact region. */
+#define RT_LAYOUT_STATS 11
 int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n);
 
 /* Validate, flatten (threaded node array, f64 payloads; rt_layout.h) and upload to `device`. */

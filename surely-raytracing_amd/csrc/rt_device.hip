@@ -210,11 +210,14 @@ int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n) {
   int rc = rtf::flatten(blob, &F, &err);
   if (rc != RT_OK) return set_err(rc, err);
   uint32_t v[RT_LAYOUT_STATS] = {(uint32_t)F.nodes.size(), F.hdr.bvh_words, 0, 0, 0, 0, 0,
-                                 F.hdr.n_lights, 0};
+                                 F.hdr.n_lights, 0, 0, F.hdr.cbvh_words * 4u};
   for (size_t p = 0; p < F.hdr.n_rec_words; p += rtf::record_words(F.nodes[p])) {
     const uint32_t h = F.nodes[p], ty = h & 0xffu;
     if (ty == RTL_BVH) ++v[2];
-    if (ty == RTL_BVH && F.nodes[p + 3] != 0u) ++v[8];
+    if (ty == RTL_BVH && F.nodes[p + 3] != 0u) {
+      ++v[8];
+      if (F.nodes[F.nodes[p + 3] + 1] != 0xffffffffu) ++v[9];
+    }
     if (ty == RTL_DUP) ++v[3];
     if (ty == RTL_VOLUME) {
       ++v[4];
@@ -452,8 +455,29 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   // BVH region (rt_layout.h): in LDS with the small scene, else staged after the Perlin tables
   // as far as the workgroup's LDS budget allows (the rest is read through the caches)
   P.bvh_words = sc->hdr.bvh_words;
+  // Compact ordered BVHs (rt_layout.h CBVH) of a product render go to LDS after the staged
+  // tables, with the walk's per-lane u16 stacks (cbvh_walk); the reference BVH region then stays
+  // in global memory (only lanes flagged for the reference-order re-walk read it)
+  P.cbvh_src = (const uint8_t*)(sc->nodes + sc->hdr.cbvh_word0);
+  P.cbvh_bytes = sc->hdr.cbvh_words * 4u;
+  P.cbvh_lds_off = ~0u;
+  P.stack_lds_off = 0;
+  size_t cbvh_lds = 0;
+  {
+    const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
+    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + (size_t)RTL_CBVH_STACK * block * 2;
+    if (bvh && !count && P.cbvh_bytes && !(opts->flags & RT_FLAG_REFERENCE_BVH) &&
+        !std::getenv("RT_NO_CBVH_LDS") && need <= cap) {
+      P.cbvh_lds_off = P.stage_bytes;
+      P.stack_lds_off = P.stage_bytes + P.cbvh_bytes;
+      cbvh_lds = need - P.stage_bytes;
+    }
+  }
   if (P.stage_scene) {
     P.bvh_lds_words = P.bvh_words;
+    P.bvh_lds_off = 0;
+  } else if (bvh && P.cbvh_lds_off != ~0u) {
+    P.bvh_lds_words = 0;
     P.bvh_lds_off = 0;
   } else if (bvh) {
     const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
@@ -467,7 +491,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.o_loffs = sc->o_loffs;
   P.o_perl = sc->o_perl;
   const size_t lds_bytes =
-      P.stage_bytes + (P.stage_scene ? 0u : (size_t)P.bvh_lds_words * 4u);
+      P.stage_bytes + (P.stage_scene ? 0u : (size_t)P.bvh_lds_words * 4u) + cbvh_lds;
   for (int k = 0; k < 3; ++k) {
     P.center[k] = cam->center[k];
     P.p00[k] = cam->pixel00_loc[k];

@@ -31,8 +31,11 @@ struct PrimBox {
 
 // rt_obvh.cpp: append an ordered BVH (rt_layout.h OBVH) for every eligible BVH subtree root in
 // `roots` (word positions of BVH records) and link it from the root's word 3.
+// Also appends the compact copies of those trees (rt_layout.h CBVH) as one region and returns
+// its first word and size in words (0, 0 when there is none).
 void build_ordered_bvhs(std::vector<uint32_t>& nodes, uint32_t rec_words,
-                        const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots);
+                        const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots,
+                        uint32_t* cbvh_word0, uint32_t* cbvh_words);
 
 // Words of the node record starting with header word h (rt_layout.h).
 uint32_t record_words(uint32_t h);

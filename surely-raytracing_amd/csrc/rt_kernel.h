@@ -305,6 +305,11 @@ struct TraceParams {
   // of them are in LDS at byte offset bvh_lds_off (staged by the prologue unless stage_scene
   // already copied the node array)
   uint32_t bvh_words, bvh_lds_words, bvh_lds_off;
+  // compact ordered BVHs (rt_layout.h CBVH) staged in LDS for cbvh_walk: cbvh_bytes from
+  // cbvh_src at LDS byte offset cbvh_lds_off (~0u: not staged, the OBVH streams are walked from
+  // global memory), and the walk's per-lane u16 stacks at stack_lds_off
+  const uint8_t* cbvh_src;
+  uint32_t cbvh_bytes, cbvh_lds_off, stack_lds_off;
   uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
@@ -1109,6 +1114,62 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
 // flag logic must see is culled.
 constexpr double kTieRel = 0x1p-30;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// The exact test of one ordered-BVH leaf record (QUAD, QUADS batch, SPHERE) with the reference
+// walker's arithmetic; every candidate goes to cand(valid, t, record).
+template <class F>
+__device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d, d3 r, double tm,
+                                          double tmin, F& cand) {
+  const uint32_t ty = N[rec] & 0xffu;
+  if (ty == RTL_SPHERE) {
+    const gptr X = N + rec;
+    d3 c = ld3(X, 0);
+    if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
+    const double rad = ldd(X, 3);
+    const d3 oc = o - c;
+    const double a = dot(d, d);
+    const double half_b = dot(oc, d);
+    const double cc = dot(oc, oc) - rad * rad;
+    const double disc = fma(half_b, half_b, -(a * cc));
+    const bool real = !(disc < 0.0);
+    const double sqrtd = sqrt_nr(disc);
+    const double ra = rcp_nr(a);
+    const double nr = (-half_b - sqrtd) * ra;
+    const double fr = (sqrtd - half_b) * ra;
+    const bool in_n = (tmin < nr) & (nr < kInf), in_f = (tmin < fr) & (fr < kInf);
+    cand(real & (in_n | in_f), in_n ? nr : fr, rec);
+  } else {
+    const bool batch = ty == RTL_QUADS;
+    const uint32_t cnt = batch ? (N[rec] >> 8) : 1u;
+    gptr Q = batch ? N + rec + 4 : N + rec;
+    uint32_t qrec = batch ? rec + 4 : rec;
+    for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS, qrec += RTL_QUAD_WORDS) {
+      const AQuad q = load_aquad(Q);
+      const uint32_t axis = RTL_QUAD_AXIS(q.h0);
+      double t, a, b, dk;
+      if (axis == 1u) {
+        aquad_core<0>(q, o, d, r, t, a, b);
+        dk = d.x;
+      } else if (axis == 2u) {
+        aquad_core<1>(q, o, d, r, t, a, b);
+        dk = d.y;
+      } else if (axis == 3u) {
+        aquad_core<2>(q, o, d, r, t, a, b);
+        dk = d.z;
+      } else {  // quad_test's arithmetic (object.rs:453-490)
+        const gptr G = Q + RTL_QUAD_GEN;
+        const d3 n = ld3(G, 0);
+        dk = dot(n, d);
+        t = div_nr(ldd(G, 3) - dot(n, o), dk);
+        const d3 pq = vfma(t, d, o) - ld3(G, 4);
+        a = dot(pq, ld3(G, 8));
+        b = dot(pq, ld3(G, 12));
+      }
+      const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+      cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & !(lo < 0.0) & !(1.0 < hi), t, qrec);
+    }
+  }
+}
+
 template <bool MAIN>
 __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double tm, int frame,
                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
@@ -1189,55 +1250,7 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
     if (e >= hd.x) break;
     const uint32_t rec = s.y;
     const double closest_before = closest;
-    const uint32_t ty = N[rec] & 0xffu;
-    if (ty == RTL_SPHERE) {
-      const gptr X = N + rec;
-      d3 c = ld3(X, 0);
-      if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
-      const double rad = ldd(X, 3);
-      const d3 oc = o - c;
-      const double a = dot(d, d);
-      const double half_b = dot(oc, d);
-      const double cc = dot(oc, oc) - rad * rad;
-      const double disc = fma(half_b, half_b, -(a * cc));
-      const bool real = !(disc < 0.0);
-      const double sqrtd = sqrt_nr(disc);
-      const double ra = rcp_nr(a);
-      const double nr = (-half_b - sqrtd) * ra;
-      const double fr = (sqrtd - half_b) * ra;
-      const bool in_n = (tmin < nr) & (nr < kInf), in_f = (tmin < fr) & (fr < kInf);
-      cand(real & (in_n | in_f), in_n ? nr : fr, rec);
-    } else {
-      const bool batch = ty == RTL_QUADS;
-      const uint32_t cnt = batch ? (N[rec] >> 8) : 1u;
-      gptr Q = batch ? N + rec + 4 : N + rec;
-      uint32_t qrec = batch ? rec + 4 : rec;
-      for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS, qrec += RTL_QUAD_WORDS) {
-        const AQuad q = load_aquad(Q);
-        const uint32_t axis = RTL_QUAD_AXIS(q.h0);
-        double t, a, b, dk;
-        if (axis == 1u) {
-          aquad_core<0>(q, o, d, r, t, a, b);
-          dk = d.x;
-        } else if (axis == 2u) {
-          aquad_core<1>(q, o, d, r, t, a, b);
-          dk = d.y;
-        } else if (axis == 3u) {
-          aquad_core<2>(q, o, d, r, t, a, b);
-          dk = d.z;
-        } else {  // quad_test's arithmetic (object.rs:453-490)
-          const gptr G = Q + RTL_QUAD_GEN;
-          const d3 n = ld3(G, 0);
-          dk = dot(n, d);
-          t = div_nr(ldd(G, 3) - dot(n, o), dk);
-          const d3 pq = vfma(t, d, o) - ld3(G, 4);
-          a = dot(pq, ld3(G, 8));
-          b = dot(pq, ld3(G, 12));
-        }
-        const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
-        cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & !(lo < 0.0) & !(1.0 < hi), t, qrec);
-      }
-    }
+    obvh_leaf(N, rec, o, d, r, tm, tmin, cand);
     if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
     ++e;
 #ifdef RT_PROF
@@ -1279,6 +1292,116 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
   return hit;
 }
 
+// The same walk over the tree's compact copy in LDS (rt_layout.h CBVH): a node holds both
+// children's boxes, both are tested in one step, the nearer hit child is visited first and the
+// other pushed on the lane's u16 stack in LDS. The box arithmetic (outward-rounded f32 bounds, the
+// octant's near/far bound per axis, the kBoxRel widening), the candidates (obvh_leaf) and the
+// tie flags are obvh_walk's, so the result is the same closest candidate and the same flag; only
+// the order of the steps and where the nodes come from differ. The LDS copy turns the walk's
+// dependent L2 round trips (~1 us each, the kernel waited on memory about half its cycles) into
+// LDS reads, and a step covers two boxes.
+template <bool MAIN>
+__device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm, int frame,
+                          double tmin, double tmax, double& t_out, uint32_t& hit_node,
+                          int& hit_frame, bool& flag) {
+  typedef const __attribute__((address_space(3))) uint8_t* lb_t;
+  typedef __attribute__((address_space(3))) uint16_t* ls_t;
+  typedef __attribute__((address_space(3))) uint8_t* lbw_t;
+  typedef const __attribute__((address_space(3))) uint32_t* lw_t;
+  const gptr N = (gptr)P.nodes;
+  const uint32_t n_int = (hd.x - 1u) >> 1;  // n_entries = 2 n_leaf - 1
+  const lb_t base = (lb_t)rt_lds + P.cbvh_lds_off + hd.y;
+  const lu4ptr nodes = reinterpret_cast<lu4ptr>(base);
+  const lw_t refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
+  const lw_t leaves = refs + n_int;
+  const ls_t stack = reinterpret_cast<ls_t>((lbw_t)rt_lds + P.stack_lds_off) + threadIdx.x;
+  const uint32_t sstride = blockDim.x;
+  const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
+  const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
+  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
+  constexpr float kBoxRel = 0x1p-20f;
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
+  const f32x2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
+  const f32x2 ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
+  const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
+  double closest = tmax;
+  float close_f = (float)(closest + closest * (2.0 * kTieRel));
+  bool hit = false;
+  double tie_at = -1.0;
+  uint32_t hn = 0;
+  auto cand = [&](bool valid, double t, uint32_t rec) {
+    const bool nt = valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel);
+    tie_at = nt ? closest : tie_at;
+    const bool win = valid & (t < closest);
+    closest = win ? t : closest;
+    hn = win ? rec : hn;
+    hit = hit | win;
+  };
+  // slab test of one child box [lo_x hi_x lo_y hi_y lo_z hi_z]: the octant's near bound per axis
+  // is hi where d_a < 0, as in the OBVH streams
+  auto box = [&](float lx, float hx, float ly, float hy, float lz, float hz, float& tn) {
+    const f32x2 bx = {lx, hx}, by = {ly, hy}, bz = {lz, hz};
+    const f32x2 tx2 = (bx - ox2) * ix2, ty2 = (by - oy2) * iy2, tz2 = (bz - oz2) * iz2;
+    const float tnx = nx ? tx2.y : tx2.x, tfx = nx ? tx2.x : tx2.y;
+    const float tny = ny ? ty2.y : ty2.x, tfy = ny ? ty2.x : ty2.y;
+    const float tnz = nz ? tz2.y : tz2.x, tfz = nz ? tz2.x : tz2.y;
+    tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
+    const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
+    return fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
+  };
+  constexpr uint32_t kDone = 0xffffu;
+  uint32_t ref = hd.z & 0xffffu;
+  uint32_t sp = 0;
+  for (;;) {
+    // while-while: steps until the lane holds a leaf whose box was hit (or is done), then the
+    // leaves with every lane that has one
+    while (ref < 0x8000u) {
+      const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
+      const uint32_t rr = refs[ref];
+      float tn0, tn1;
+      const bool h0 = box(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
+                          __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y), tn0);
+      const bool h1 = box(__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x),
+                          __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w), tn1);
+      const bool first0 = h0 & (!h1 | (tn0 <= tn1));
+      const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
+      if (h0 & h1) {
+        stack[sp * sstride] = (uint16_t)(first0 ? r1 : r0);
+        ++sp;
+      }
+      if (h0 | h1) {
+        ref = first0 ? r0 : r1;
+      } else if (sp > 0) {
+        --sp;
+        ref = stack[sp * sstride];
+      } else {
+        ref = kDone;
+      }
+    }
+    if (ref == kDone) break;
+    const double closest_before = closest;
+    obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin, cand);
+    if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
+    if (sp > 0) {
+      --sp;
+      ref = stack[sp * sstride];
+    } else {
+      ref = kDone;
+    }
+  }
+  flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
+         (hit & (closest <= tmin * (1.0 + kTieRel)));
+  if (hit) {
+    t_out = closest;
+    if (MAIN) {
+      hit_node = hn;
+      hit_frame = frame;
+    }
+  }
+  return hit;
+}
+
 template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
@@ -1300,8 +1423,13 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
   if constexpr (!COUNT) {
     if (obvh != 0u && !(P.flags & RT_FLAG_REFERENCE_BVH)) {
       bool flag = false;
-      bool h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,
-                               flag);
+      const uint4 hd = ld4u((gptr)P.nodes + obvh);  // [n_entries][cbvh block][root ref][streams]
+      bool h;
+      if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
+        h = cbvh_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
+      else
+        h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,
+                            flag);
       if (__ballot(flag) != 0ull && flag)  // rare: the reference order decides
         h = traverse<MAIN, COUNT, VOLB, false, BVH>(P, node, stop, wo, wd, tm, o, d, frame, tmin,
                                                     tmax, t_out, hit_node, hit_frame, g, C);
@@ -1636,7 +1764,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     for (int k = threadIdx.x; k < RT_OP_COUNT; k += blockDim.x) sh_ops[k] = 0u;
     __syncthreads();
   }
-  if (P.stage_bytes || (BVH && !P.stage_scene && P.bvh_lds_words)) {
+  if (P.stage_bytes || (BVH && !P.stage_scene && P.bvh_lds_words) ||
+      (BVH && !COUNT && P.cbvh_lds_off != ~0u)) {
     // copy the small tables (or just the Perlin tables) into LDS, then the BVH region
     const uint4* src = reinterpret_cast<const uint4*>(P.stage_src);
     uint4* dst = reinterpret_cast<uint4*>(rt_lds);
@@ -1647,6 +1776,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       uint4* bdst = reinterpret_cast<uint4*>(rt_lds + P.bvh_lds_off);
       const uint32_t b16 = P.bvh_lds_words / 4;
       for (uint32_t k = threadIdx.x; k < b16; k += blockDim.x) bdst[k] = bsrc[k];
+    }
+    if (BVH && !COUNT && P.cbvh_lds_off != ~0u) {
+      const uint4* csrc = reinterpret_cast<const uint4*>(P.cbvh_src);
+      uint4* cdst = reinterpret_cast<uint4*>(rt_lds + P.cbvh_lds_off);
+      for (uint32_t k = threadIdx.x; k < P.cbvh_bytes / 16; k += blockDim.x) cdst[k] = csrc[k];
     }
     __syncthreads();
   }

@@ -88,7 +88,15 @@
  *   [skip][0][near_x][far_x][near_y][far_y][near_z][far_z] (f32 bounds of the node's box for the
  *   octant, outward-rounded with margin: box hit -> next entry, miss -> skip); leaf entry:
  *   [0x80000000][record][the leaf's own box, as above] (box hit -> test the record; then the
- *   next entry). */
+ *   next entry). Header words 1-2: the tree's block in the CBVH region (byte offset, 0xffffffff =
+ *   none) and its root reference.
+ * CBVH: the same trees, compact, for the walk from LDS (rt_kernel.h cbvh_walk): one contiguous
+ *   region after the OBVHs (header cbvh_word0 / cbvh_words) of 16-byte aligned blocks, one per
+ *   tree: n_int internal nodes of 48 bytes (both children's boxes as f32 [lo_x hi_x lo_y hi_y
+ *   lo_z hi_z], outward-rounded as above), n_int u32 child-reference pairs (ref0 | ref1 << 16;
+ *   ref < 0x8000: internal node, else leaf index ref & 0x7fff), n_int + 1 u32 leaf records.
+ *   Internal-node depth <= RTL_CBVH_STACK (the walk's per-lane stack). */
+#define RTL_CBVH_STACK 24
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
@@ -151,4 +159,6 @@ typedef struct rtl_scene_header {
   uint32_t n_rec_words;   /* node words holding records; ordered BVHs follow (OBVH below) */
   uint32_t lights_nested; /* some light entry is a nested HittableList (RTL_LLIST)    */
   uint32_t nested_volumes;/* a ConstantMedium lies inside another one's boundary      */
+  uint32_t cbvh_word0;    /* CBVH region (below): first node word, 0 = none            */
+  uint32_t cbvh_words;    /* its size in words (a multiple of 4)                        */
 } rtl_scene_header;

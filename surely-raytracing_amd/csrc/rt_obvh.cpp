@@ -157,8 +157,85 @@ bool collect(const std::vector<uint32_t>& w, uint32_t x, const std::vector<PrimB
 
 }  // namespace
 
+// Outward-rounded f32 bounds of a node's box (the padded f64 box grown by 2^-18 (1 + |coord|)):
+// rt_kernel.h obvh_walk / cbvh_walk's error budget.
+void f32_box(const BNode& n, float lo[3], float hi[3]) {
+  for (int a = 0; a < 3; ++a) {
+    const double m = 0x1p-18 * (1.0 + std::max(std::fabs(n.lo[a]), std::fabs(n.hi[a])));
+    lo[a] = f32_down(n.lo[a] - m);
+    hi[a] = f32_up(n.hi[a] + m);
+  }
+}
+
+// The compact copy of one tree (rt_layout.h CBVH) as words; false when it does not fit the
+// format (16-bit references, internal-node depth <= RTL_CBVH_STACK).
+bool compact_tree(const std::vector<BNode>& nodes, const std::vector<Leaf>& leaves,
+                  std::vector<uint32_t>* out, uint32_t* root_ref) {
+  const size_t n_leaf = leaves.size();
+  if (n_leaf == 0 || n_leaf > 0x7fffu) return false;
+  if (n_leaf == 1) {  // a single leaf: the root reference is the leaf
+    out->assign(4, 0u);
+    (*out)[0] = leaves[0].rec;
+    *root_ref = 0x8000u;
+    return true;
+  }
+  // internal nodes in pre-order (index 0 = the root), leaves in first-visit order
+  std::vector<int> order, leaf_of(nodes.size(), -1), int_of(nodes.size(), -1);
+  std::vector<uint32_t> leaf_recs;
+  int max_depth = 0;
+  struct Walk {
+    const std::vector<BNode>& N;
+    const std::vector<Leaf>& L;
+    std::vector<int>& order;
+    std::vector<int>& leaf_of;
+    std::vector<int>& int_of;
+    std::vector<uint32_t>& recs;
+    int& max_depth;
+    void run(int i, int depth) {
+      if (N[i].left < 0) {
+        leaf_of[i] = (int)recs.size();
+        recs.push_back(L[N[i].right].rec);
+        return;
+      }
+      max_depth = std::max(max_depth, depth);
+      int_of[i] = (int)order.size();
+      order.push_back(i);
+      run(N[i].left, depth + 1);
+      run(N[i].right, depth + 1);
+    }
+  } wk{nodes, leaves, order, leaf_of, int_of, leaf_recs, max_depth};
+  wk.run(0, 1);
+  const size_t n_int = order.size();
+  if (n_int > 0x7fffu || max_depth > RTL_CBVH_STACK || leaf_recs.size() != n_leaf) return false;
+  auto ref = [&](int c) -> uint32_t {
+    return nodes[c].left < 0 ? 0x8000u | (uint32_t)leaf_of[c] : (uint32_t)int_of[c];
+  };
+  const size_t words = (n_int * 12 + n_int + n_leaf + 3) & ~(size_t)3;
+  out->assign(words, 0u);
+  uint32_t* B = out->data();
+  for (size_t k = 0; k < n_int; ++k) {
+    const BNode& n = nodes[order[k]];
+    const int ch[2] = {n.left, n.right};
+    for (int c = 0; c < 2; ++c) {
+      float lo[3], hi[3];
+      f32_box(nodes[ch[c]], lo, hi);
+      for (int a = 0; a < 3; ++a) {
+        std::memcpy(&B[k * 12 + c * 6 + 2 * a], &lo[a], 4);
+        std::memcpy(&B[k * 12 + c * 6 + 2 * a + 1], &hi[a], 4);
+      }
+    }
+    B[n_int * 12 + k] = ref(n.left) | ref(n.right) << 16;
+  }
+  for (size_t k = 0; k < n_leaf; ++k) B[n_int * 13 + k] = leaf_recs[k];
+  *root_ref = 0u;
+  return true;
+}
+
 void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
-                        const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots) {
+                        const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots,
+                        uint32_t* cbvh_word0, uint32_t* cbvh_words) {
+  std::vector<uint32_t> cbvh;  // the compact region, appended after every ordered stream
+  *cbvh_word0 = *cbvh_words = 0u;
   for (uint32_t root : roots) {
     std::vector<Leaf> leaves;
     if (!collect(w, root, boxes, leaves, 0) || leaves.empty() || leaves.size() > (1u << 20))
@@ -203,20 +280,32 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
             run(neg ? n.left : n.right);
             E[0] = pos;  // skip: the entry after the subtree
           }
-          for (int a = 0; a < 3; ++a) {  // the node's (or leaf's) own box
-            // conservative f32 bounds: the padded f64 box grown by 2^-18 (1 + |coord|) and
-            // rounded outwards (rt_kernel.h obvh_walk's error budget)
-            const double m = 0x1p-18 * (1.0 + std::max(std::fabs(n.lo[a]), std::fabs(n.hi[a])));
-            const float lo = f32_down(n.lo[a] - m), hi = f32_up(n.hi[a] + m);
+          float lo[3], hi[3];  // the node's (or leaf's) own box, conservative f32 bounds
+          f32_box(n, lo, hi);
+          for (int a = 0; a < 3; ++a) {
             const bool na = (oct >> a) & 1u;  // d_a < 0: the near bound is hi
-            std::memcpy(&E[2 + 2 * a], na ? &hi : &lo, 4);
-            std::memcpy(&E[3 + 2 * a], na ? &lo : &hi, 4);
+            std::memcpy(&E[2 + 2 * a], na ? &hi[a] : &lo[a], 4);
+            std::memcpy(&E[3 + 2 * a], na ? &lo[a] : &hi[a], 4);
           }
         }
       } em{B.nodes, leaves, S, oct, pos};
       em.run(0);
     }
     w[root + 3] = hdr;  // the reference BVH record points at its ordered tree
+    std::vector<uint32_t> blk;
+    uint32_t root_ref = 0u;
+    w[hdr + 1] = 0xffffffffu;
+    if (!std::getenv("RT_NO_CBVH") && compact_tree(B.nodes, leaves, &blk, &root_ref)) {
+      w[hdr + 1] = (uint32_t)(cbvh.size() * 4);  // byte offset in the region
+      w[hdr + 2] = root_ref;
+      cbvh.insert(cbvh.end(), blk.begin(), blk.end());
+    }
+  }
+  if (!cbvh.empty()) {
+    while (w.size() % 4) w.push_back(0u);
+    *cbvh_word0 = (uint32_t)w.size();
+    *cbvh_words = (uint32_t)cbvh.size();
+    w.insert(w.end(), cbvh.begin(), cbvh.end());
   }
   (void)rec_words;
 }

@@ -489,7 +489,8 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
 
 
 LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
-                "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs"]
+                "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs",
+                "compact_bvhs", "compact_bvh_bytes"]
 
 
 def render_multi(blob: "Blob", cam: RtCamera, opts: RtRenderOpts, devices,

@@ -71,3 +71,19 @@ def test_ordered_bvhs_for_primitive_leaf_subtrees():
     world = sc.hittable_list(sc.create_bvh(items))
     st = rt.layout_stats(sc.serialize(world, None))
     assert st["bvh_records"] > 0 and st["ordered_bvhs"] == 0
+
+
+def test_compact_bvhs_fit_the_lds_budget():
+    """rt_obvh.cpp / rt_layout.h CBVH: both final_scene trees also get the compact copy that
+    cbvh_walk reads from LDS (48-byte two-child nodes, u16 references, internal depth <= 24),
+    and with the per-lane stacks of a 768-thread workgroup (24 levels x 2 bytes), the f64 sample
+    sums and the Perlin table it fits the CU's 160 KiB."""
+    blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
+    st = rt.layout_stats(blob)
+    assert st["compact_bvhs"] == st["ordered_bvhs"] == 2
+    n_leaves = 400 + 1000
+    n_int = n_leaves - 2
+    assert st["compact_bvh_bytes"] >= n_int * 52 + n_leaves * 4
+    assert st["compact_bvh_bytes"] <= n_int * 52 + n_leaves * 4 + 2 * 16
+    stacks, sums, perlin = 24 * 768 * 2, 768 * 24, 8960
+    assert st["compact_bvh_bytes"] + stacks + sums + perlin + 512 <= 160 * 1024
