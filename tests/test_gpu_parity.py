@@ -437,6 +437,20 @@ def test_chunked_and_tail_split_renders_are_bitwise_equal(gpu_available, name, k
         assert np.array_equal(one, other, equal_nan=True), env
 
 
+def test_bvh_walks_from_lds_global_and_reference_order_are_bitwise_equal(gpu_available):
+    """final_scene at depth 40: the compact ordered BVHs walked from LDS (cbvh_walk, the product
+    default), the per-octant ordered streams walked from global memory (RT_NO_CBVH_LDS) and the
+    reference tree in the reference order (RT_FLAG_REFERENCE_BVH, hittable.rs:216-236) return
+    the same records, so the three images are equal bit for bit."""
+    blob, cam = rt.preset_blob("final_scene", width=96, spp=16, depth=40)
+    assert rt.layout_stats(blob)["compact_bvhs"] == 2
+    lds = _render_env(blob, cam, {})
+    streams = _render_env(blob, cam, {"RT_NO_CBVH_LDS": 1})
+    ref = _render_env(blob, cam, {}, flags=rt.RT_FLAG_OVERWRITE | rt.RT_FLAG_REFERENCE_BVH)
+    assert np.array_equal(lds, streams, equal_nan=True)
+    assert np.array_equal(lds, ref, equal_nan=True)
+
+
 def _zero_pdf_scene():
     """A floor whose light-sampled bounces have pdf_val = 0 exactly, and whose sub-paths then
     return 0. The light list holds a quad 1e-9 below the floor's plane (not in the world): a
