@@ -180,8 +180,7 @@ bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostri
     const uint32_t cnt = batch ? (N[x] >> 8) : 1u;
     const size_t q0 = batch ? x + 4 : x;
     b << "    const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));\n"
-         "    double m1 = 0.0, m2 = 0.0;\n"
-         "    bool have1 = false, have2 = false;\n";
+         "    double m1 = kInf, m2 = kInf;  // the two smallest candidates, +inf = none\n";
     static const char* ax = "xyz";
     for (uint32_t k = 0; k < cnt; ++k) {
       const size_t q = q0 + (size_t)k * RTL_QUAD_WORDS;
@@ -195,14 +194,12 @@ bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostri
         << "      const double dk = d." << ax[K] << ";\n"
            "      const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);\n"
            "      const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);\n"
-           "      const bool lt1 = v & (!have1 | (t < m1));\n"
-           "      const bool lt2 = v & !lt1 & (!have2 | (t < m2));\n"
-           "      m2 = lt1 ? m1 : (lt2 ? t : m2);\n"
-           "      have2 = have2 | (lt1 & have1) | lt2;\n"
-           "      m1 = lt1 ? t : m1;\n"
-           "      have1 = have1 | v;\n    }\n";
+           "      const double te = v ? t : kInf;\n"
+           "      m2 = __builtin_fmin(m2, __builtin_fmax(m1, te));\n"
+           "      m1 = __builtin_fmin(m1, te);\n    }\n";
     }
-    b << "    t1 = m1;\n"
+    b << "    const bool have1 = m1 < kInf, have2 = m2 < kInf;\n"
+         "    t1 = m1;\n"
          "    const double tmin2 = m1 + 0.0001;\n"
          "    bool hit2;\n"
          "    if (m1 >= tmin2) {\n      t2 = m1;\n      hit2 = true;\n"

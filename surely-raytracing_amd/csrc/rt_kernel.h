@@ -710,8 +710,9 @@ __device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t ki
   const uint32_t cnt = batch ? (X[0] >> 8) : 1u;
   kptr Q = batch ? X + 4 : X;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
-  double m1 = 0.0, m2 = 0.0;
-  bool have1 = false, have2 = false;
+  // the two smallest candidates with multiplicity, +inf = none: min/max updates (a candidate's t
+  // is finite: |q_k - o_k| < 2^1023 and |d_k| >= 1e-8)
+  double m1 = kInf, m2 = kInf;
   for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
     const AQuad q = load_aquad(Q);
     double t, a, b;
@@ -724,13 +725,11 @@ __device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t ki
     const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
     // aquad_test's predicate without the interval, plus t >= -inf (not NaN)
     const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);
-    const bool lt1 = v & (!have1 | (t < m1));
-    const bool lt2 = v & !lt1 & (!have2 | (t < m2));
-    m2 = lt1 ? m1 : (lt2 ? t : m2);
-    have2 = have2 | (lt1 & have1) | lt2;
-    m1 = lt1 ? t : m1;
-    have1 = have1 | v;
+    const double te = v ? t : kInf;
+    m2 = __builtin_fmin(m2, __builtin_fmax(m1, te));
+    m1 = __builtin_fmin(m1, te);
   }
+  const bool have1 = m1 < kInf, have2 = m2 < kInf;
   t1 = m1;
   const double tmin2 = m1 + 0.0001;
   bool hit2;
