@@ -323,6 +323,7 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
 void rt_scene_destroy(rt_scene* sc) {
   if (!sc) return;
   (void)hipSetDevice(sc->device);
+  for (const rtj::Kernel& k : sc->jit_k) rtj::release_kernel(k);  // the module cache's holds
   if (sc->dev) (void)hipFree(sc->dev);
   if (sc->work) (void)hipFree(sc->work);
   if (sc->ops) (void)hipFree(sc->ops);
@@ -595,6 +596,7 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
             (size_t)jk.static_lds > static_lds) {
           sc->jit_state = -2;
           sc->jit_msg = std::string("not launched: ") + why;
+          rtj::release_kernel(jk);
           jk = rtj::Kernel{};
         } else {
           sc->jit_msg = why;

@@ -634,16 +634,59 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   return 0;
 }
 
+namespace {
+// The module cache: per (device, source) the kernel, the number of scenes holding it and the
+// time of its last hand-out (for evicting the least recently used unheld modules).
+struct Entry {
+  Kernel k;
+  int holds = 0;
+  uint64_t used = 0;
+};
+std::mutex g_mu;
+std::map<std::pair<int, std::string>, Entry> g_cache;
+uint64_t g_tick = 0;
+
+void evict_idle_locked() {
+  for (;;) {
+    int idle = 0;
+    auto oldest = g_cache.end();
+    for (auto it = g_cache.begin(); it != g_cache.end(); ++it) {
+      if (it->second.holds > 0) continue;
+      ++idle;
+      if (oldest == g_cache.end() || it->second.used < oldest->second.used) oldest = it;
+    }
+    if (idle <= kIdleModules) return;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(oldest->first.first);
+    (void)hipModuleUnload(oldest->second.k.mod);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    g_cache.erase(oldest);
+  }
+}
+}  // namespace
+
+void release_kernel(const Kernel& k) {
+  if (!k.mod) return;
+  std::lock_guard<std::mutex> lock(g_mu);
+  for (auto& kv : g_cache)
+    if (kv.second.k.mod == k.mod && kv.second.holds > 0) {
+      --kv.second.holds;
+      break;
+    }
+  evict_idle_locked();
+}
+
 int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
                std::string* log) {
-  static std::mutex mu;
-  static std::map<std::pair<int, std::string>, Kernel> cache;
   const std::string s = kernel_source(walker, f);
-  std::lock_guard<std::mutex> lock(mu);
+  std::lock_guard<std::mutex> lock(g_mu);
   auto key = std::make_pair(device, s);
-  auto it = cache.find(key);
-  if (it != cache.end()) {
-    *out = it->second;
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) {
+    ++it->second.holds;
+    it->second.used = ++g_tick;
+    *out = it->second.k;
     return 0;
   }
   hipDeviceProp_t prop;
@@ -671,7 +714,11 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
     *log = "hipFuncGetAttribute failed on the scene-specialised kernel";
     return RT_ERR_HIP;
   }
-  cache.emplace(key, k);
+  Entry e;
+  e.k = k;
+  e.holds = 1;
+  e.used = ++g_tick;
+  g_cache.emplace(key, e);
   *out = k;
   return 0;
 }

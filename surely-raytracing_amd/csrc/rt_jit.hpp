@@ -36,6 +36,11 @@ struct Kernel {
 };
 int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
                std::string* log);
+// A scene's hold on a kernel from get_kernel ends (rt_scene_destroy). The process-wide cache keeps
+// every kernel some scene holds, plus up to kIdleModules unheld ones for scenes created again
+// with the same geometry; older unheld modules are unloaded (hipModuleUnload).
+constexpr int kIdleModules = 8;
+void release_kernel(const Kernel& k);
 
 // The hiprtc translation unit (embedded headers + walker + rt_trace_jit wrapper) and its
 // compilation for `arch` (e.g. "gfx950") into a code object; host-only, no device needed.

@@ -1354,7 +1354,9 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   uint32_t sp = 0;
   for (;;) {
     // while-while: steps until the lane holds a leaf whose box was hit (or is done), then the
-    // leaves with every lane that has one
+    // leaves with every lane that has one. (Postponing a lane's leaf and stepping on until every
+    // lane holds one -- speculative while-while -- was 11 % slower at C4: more steps against an
+    // older closest t.)
     while (ref < 0x8000u) {
       const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
       const uint32_t rr = refs[ref];
