@@ -1950,6 +1950,24 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       }
     }
     next += __popcll(want);
+#ifdef RT_ABL_FRESH2  // ablation build: a second, discarded camera ray per fresh lane (its cost)
+    if (fresh) {
+      const kparams_t Q = kparams();
+      uint32_t xk2 = xk;
+      asm volatile("" : "+v"(xk2));
+      const int x = (int)(xk2 & 0xffffu);
+      const int y = Q->row_begin + (int)((xk2 >> 16) & 0x7fffu) * Q->row_step;
+      const int s_i = (int)(sij & 0xffffu), s_j = (int)(sij >> 16);
+      Rng g2 = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
+                        (uint32_t)(s_j * Q->sqrt_spp + s_i));
+      d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
+      double px = fma(Q->rs, (double)s_i + rnd(g2), -0.5);
+      double py = fma(Q->rs, (double)s_j + rnd(g2), -0.5);
+      d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
+      const double t2 = rnd(g2);
+      asm volatile("" ::"v"(ps.x), "v"(ps.y), "v"(ps.z), "v"(t2));
+    }
+#endif
     if (fresh) {
       const kparams_t Q = kparams();
       const int x = (int)(xk & 0xffffu);
