@@ -356,6 +356,7 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
        "    d3 o = ro, d = rd;\n";
   size_t node = F.hdr.root;
   int frame = -1;
+  bool wlen = false;  // |rd| emitted for the world frame's volumes
   for (size_t guard = 0;; ++guard) {
     if (node + 4 > N.size() || guard > N.size()) {
       *why = "malformed node sequence";
@@ -390,13 +391,18 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
       }
       node = N[node + 3];
     } else if (ty == RTL_VOLUME) {
-      // ConstantMedium (constant_medium.rs:41-95): the interpreter's boundary walks
+      // ConstantMedium (constant_medium.rs:41-95): the interpreter's boundary walks; the world
+      // frame's volumes share one |rd| (constant_medium.rs:73 r.direction().length())
       const bool vt = gen_volume_two_hits(N, node, pre);
+      if (frame < 0 && !wlen) {
+        o << "    const double wlen = sqrt_nr(dot(rd, rd));\n";
+        wlen = true;
+      }
       o << "    h = volume_hit<COUNT, true, BVH, VOLI"
         << (vt ? ", VolTwo_" + std::to_string(node) : std::string()) << ">(P, " << node
         << "u, make_uint4(" << N[node] << "u, "
         << N[node + 1] << "u, " << N[node + 2] << "u, " << N[node + 3] << "u), ro, rd, tm, o, d, "
-        << frame << ", tmin, closest, t, g, C);\n"
+        << frame << ", tmin, closest, t, g, C" << (frame < 0 ? ", &wlen" : "") << ");\n"
         << "    closest = h ? t : closest;\n    code = h ? " << G.code(node, frame) << "u : code;\n";
       ++G.prims;
       node = N[node + 1];

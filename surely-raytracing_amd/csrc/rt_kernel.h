@@ -814,7 +814,10 @@ __device__ bool traverse(const TraceParams& P, uint32_t node, uint32_t stop, d3 
 template <bool COUNT, bool UNI, bool BVH, bool VOLI, class VT = VolTwoInterp, int VN = 0>
 __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, uint4 h, d3 wo,
                                            d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
-                                           double closest, double& t_hit, Rng& g, Ctr<COUNT>& C) {
+                                           double closest, double& t_hit, Rng& g, Ctr<COUNT>& C,
+                                           const double* ray_len = nullptr) {
+  // ray_len: |d| computed once by a generated walker for all the volumes of one frame (the same
+  // sqrt_nr(dot(d, d)) of the same d)
   typedef typename cond<UNI, kptr, gptr>::type Ptr;
   const Ptr X = (Ptr)P.nodes + node;
   C.inc(RT_OP_VOLUME_TESTS);
@@ -861,7 +864,7 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
     if (t2 > closest) t2 = closest;
     if (t1 < t2) {
       if (t1 < 0.0) t1 = 0.0;
-      double ray_length = sqrt_nr(dot(d, d));
+      const double ray_length = ray_len ? *ray_len : sqrt_nr(dot(d, d));
       double dist_inside = (t2 - t1) * ray_length;
       C.inc(RT_OP_VOLUME_DRAWS);
       double hit_distance = ldd(X, 0) * log_u01(rnd(g));
