@@ -76,6 +76,31 @@ def test_cornell_c1_parity(gpu_available):
     assert acc_g.mean() > 0.05
 
 
+@pytest.mark.parametrize("name,kw", [
+    ("cornell_box", dict(width=61, spp=9)),
+    ("final_scene", dict(width=45, spp=4, depth=12, aspect=16.0 / 9.0)),
+])
+def test_ragged_tiles_parity(gpu_available, name, kw):
+    """Image widths and heights that are not multiples of the 8x8 pool tile: the right-edge
+    tiles decode their pixels by division (the full-width tiles by shifts) and the bottom tiles
+    hold fewer rows; every pixel is still rendered once, against the oracle."""
+    blob, cam = rt.preset_blob(name, **kw)
+    assert cam.image_width % 8 != 0
+    acc_g, acc_o, st = _compare(blob, cam, ops_rtol=1e-4 if name == "final_scene" else 0.0)
+    assert st.samples == cam.image_width * cam.image_height * cam.samples_per_pixel
+
+
+def test_max_depth_zero_renders_black(gpu_available):
+    """ray_color's depth guard at depth 0 (render.rs:260-262): every sample returns black
+    without a world query (the camera-ray block ends it; op counts as the oracle's)."""
+    blob, cam = rt.preset_blob("cornell_box", width=24, spp=4)
+    cam.max_depth = 0
+    acc_g, acc_o, st = _compare(blob, cam)
+    assert not acc_g.any() and not acc_o.any()
+    ops = st.op_counts()
+    assert ops["world_queries"] == 0 and ops["depth_cutoff"] == ops["samples"] == 24 * 24 * 4
+
+
 @pytest.mark.parametrize("name,variant,width,spp,depth", [
     ("cornell_box", "mixed_pdf", 96, 16, 50),
     ("cornell_smoke", "", 96, 9, 10),
