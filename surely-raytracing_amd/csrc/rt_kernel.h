@@ -2079,11 +2079,13 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     const TP M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
     uint4 mh = ld4u(M);
     const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
+    // the primitive's outward normal per type, then ONE set_face_normal (hittable.rs:22-37) for
+    // every lane; a ConstantMedium hit has normal (1, 0, 0) and front_face true
+    // (constant_medium.rs:82-90)
+    d3 outward;
     if (type == RTL_QUAD) {
       const TP XG = X + RTL_QUAD_GEN;
-      d3 n = ld3(XG, 0);
-      front = dot(d, n) < 0.0;  // set_face_normal hittable.rs:22-37
-      normal = front ? n : -n;
+      outward = ld3(XG, 0);
       if (needs_uv) {
         d3 pq = p - ld3(XG, 4);
         u = dot(pq, ld3(XG, 8));
@@ -2092,13 +2094,13 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     } else if (type == RTL_SPHERE) {
       d3 c = ld3(X, 0);
       if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
-      d3 outward = (p - c) * ldd(X, 7);
-      front = dot(d, outward) < 0.0;
-      normal = front ? outward : -outward;
+      outward = (p - c) * ldd(X, 7);
       if (needs_uv) sphere_uv(outward, u, v);
-    } else {  // volume (constant_medium.rs:82-90)
-      normal = mk(1., 0., 0.);
+    } else {
+      outward = mk(1., 0., 0.);
     }
+    front = (type != RTL_QUAD && type != RTL_SPHERE) | (dot(d, outward) < 0.0);
+    normal = front ? outward : -outward;
     Trav::frame_out(T.nodes, hf, p, normal);  // back to world space
     const uint32_t kind = mh.x & 0xffu;
     PROF(3);
