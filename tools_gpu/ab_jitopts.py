@@ -9,8 +9,12 @@ import sys
 scene, W, SPP = sys.argv[1], sys.argv[2], sys.argv[3]
 SETS = ["", "-mllvm -amdgpu-sched-strategy=iterative-minreg", "-mllvm -misched=ilpmin",
         "-mllvm -amdgpu-sched-strategy=max-ilp", "-mllvm -misched=ilpmax", ""]
+if os.environ.get("AB_SETS"):  # ';'-separated option sets (the default runs first and last)
+    SETS = [""] + [x.strip() for x in os.environ["AB_SETS"].split(";")] + [""]
 CHILD = r"""
-import sys, hashlib
+import sys, hashlib, os
+if os.environ.get("AB_TORCH", "1") == "1":
+    import torch  # as bench.py: torch's bundled hiprtc builds the scene kernels
 sys.path.insert(0, "surely-raytracing_amd")
 import numpy as np, surely_rt as rt
 blob, cam = rt.preset_blob(sys.argv[1], width=int(sys.argv[2]), spp=int(sys.argv[3]))
