@@ -1175,6 +1175,20 @@ EXPORT void oracle_rng_u32(uint64_t seed, uint32_t pixel, uint32_t sample, int n
   for (int i = 0; i < n; ++i) out[i] = rng_u32(&g);
 }
 /* get_sphere_uv (object.rs:114-120) at unit-sphere points p[3*i..] -> uv[2*i..] */
+/* Perlin::turb (perlin.rs:56-72 over noise 30-54 and trilinear_interp 74-96) of one table:
+ * ranvec 256 x 3 doubles, perms 3 x 256 (perm_x, perm_y, perm_z), n points. KAT entry. */
+EXPORT void oracle_perlin_turb(const double* ranvec, const int* perms, const double* pts, int n,
+                               double* out) {
+  operlin pl;
+  for (int k = 0; k < 256; ++k) {
+    pl.ranvec[k] = v3(R(ranvec[3 * k]), R(ranvec[3 * k + 1]), R(ranvec[3 * k + 2]));
+    pl.px[k] = perms[k];
+    pl.py[k] = perms[256 + k];
+    pl.pz[k] = perms[512 + k];
+  }
+  for (int i = 0; i < n; ++i)
+    out[i] = (double)perlin_turb(NULL, &pl, v3(R(pts[3 * i]), R(pts[3 * i + 1]), R(pts[3 * i + 2])));
+}
 EXPORT void oracle_sphere_uv(const double* p, int n, double* uv) {
   for (int i = 0; i < n; ++i) {
     real u, v;

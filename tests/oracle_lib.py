@@ -34,6 +34,7 @@ def lib(precision: int = 32) -> C.CDLL:
         L.oracle_rng_draws.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
         L.oracle_rng_u32.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p]
         L.oracle_sphere_uv.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_perlin_turb.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_light_pdf_batch.restype = C.c_int
         L.oracle_light_pdf_batch.argtypes = [C.POINTER(RtSceneBlob), C.c_void_p, C.c_void_p, C.c_int,
                                              C.c_void_p]

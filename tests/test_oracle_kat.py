@@ -248,3 +248,59 @@ def test_f32_study_math_accuracy(fn):
     ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
     err = np.abs(got - ref) / np.maximum(ulp, np.spacing(np.float32(1e-3)))
     assert err.max() < 8, err.max()
+
+
+def _turb_reference(ranvec, perms, p):
+    """perlin.rs:30-96 restated line by line in Python floats (f64, the reference's order)."""
+    def sat_i32(f):
+        if f != f:
+            return 0
+        return int(max(-2147483648.0, min(2147483647.0, f)))
+
+    def noise(p):
+        u = p[0] - math.floor(p[0])
+        v = p[1] - math.floor(p[1])
+        w = p[2] - math.floor(p[2])
+        i, j, k = sat_i32(math.floor(p[0])), sat_i32(math.floor(p[1])), sat_i32(math.floor(p[2]))
+        c = [[[ranvec[perms[0][(i + di) & 255] ^ perms[1][(j + dj) & 255] ^ perms[2][(k + dk) & 255]]
+               for dk in range(2)] for dj in range(2)] for di in range(2)]
+        return trilinear_interp(c, u, w, v)
+
+    def trilinear_interp(c, u, w, v):
+        uu = u * u * (3. - 2. * u)
+        vv = v * v * (3. - 2. * v)
+        ww = w * w * (3. - 2. * w)
+        accum = 0.
+        for i in range(2):
+            for j in range(2):
+                for k in range(2):
+                    cv = c[i][j][k]
+                    wv = (u - i, v - j, w - k)
+                    d = (cv[0] * wv[0] + cv[1] * wv[1]) + cv[2] * wv[2]  # vec3.rs:168
+                    accum += ((i * uu + (1. - i) * (1. - uu)) * (j * vv + (1. - j) * (1. - vv))
+                              * (k * ww + (1. - k) * (1. - ww)) * d)
+        return accum
+
+    accum, weight, tp = 0., 1., list(p)
+    for _ in range(7):  # turb_depth(p, 7)
+        accum += weight * noise(tp)
+        weight *= 0.5
+        tp = [x * 2. for x in tp]
+    return abs(accum)
+
+
+def test_perlin_turb_matches_the_reference_formulas():
+    """Perlin::turb (perlin.rs:56-72; noise 30-54, trilinear_interp 74-96), the noise texture
+    of C4's marble sphere (texture.rs:127-130): the f64 oracle equals a line-by-line Python
+    restatement bit for bit, on random tables and points incl. negative coordinates."""
+    rng = np.random.default_rng(11)
+    ranvec = rng.normal(size=(256, 3))
+    ranvec /= np.linalg.norm(ranvec, axis=1, keepdims=True)
+    perms = np.stack([rng.permutation(256) for _ in range(3)]).astype(np.int32)
+    pts = np.concatenate([rng.uniform(-300, 300, size=(200, 3)), rng.uniform(-2, 2, size=(56, 3))])
+    out = np.zeros(len(pts))
+    O.lib(64).oracle_perlin_turb(ranvec.ctypes.data, perms.ctypes.data, pts.ctypes.data, len(pts),
+                                 out.ctypes.data)
+    ref = [_turb_reference(ranvec.tolist(), perms.tolist(), p) for p in pts.tolist()]
+    assert np.array_equal(out, np.array(ref))
+    assert 0.0 < out.mean() < 2.0
