@@ -13,8 +13,9 @@
 // and takes a segment item (one pixel's samples of the block, summed in f64 in LDS) or, for the
 // launch's last pools, one sample; when its item ends it writes the f64 partial and claims the
 // next item with a wave ballot + mbcnt, so lanes stay busy whatever the per-pixel path cost.
-// rt_reduce sums the partials in the reference's order (s_i inside s_j, render.rs:185-189) into
-// the caller's accumulator, so no atomics touch the framebuffer and results are bitwise
+// rt_reduce adds the f64 block partials in the reference's sample order (s_i inside s_j,
+// render.rs:185-189; the association differs from its single running sum only between blocks
+// of kPoolSi samples) into the caller's accumulator, so no atomics touch the framebuffer and results are bitwise
 // reproducible and identical across 1..8 GPUs (the RNG is keyed by global pixel and sample).
 #include <hip/hip_runtime.h>
 
