@@ -124,10 +124,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # RT_BENCH_REHEARSAL=1: the N > 1 code path on a one-GPU box (gloo, every rank on the same
+    # card, the gather through host memory); the driver's multi-GPU runs use RCCL, one GPU a rank
+    rehearse = os.environ.get("RT_BENCH_REHEARSAL") == "1"
+    local = local % torch.cuda.device_count() if rehearse else local
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     blob, cam = rt.preset_blob(args.scene, width=args.width, spp=args.spp, depth=args.depth,
                                aspect=args.aspect)
@@ -146,7 +153,7 @@ def main():
         ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        return gather_frame(local_buf, H, rank, world)
+        return gather_frame(local_buf.cpu() if rehearse else local_buf, H, rank, world)
 
     # ---- op counts for the roofline (outside the timed region; deterministic)
     ops = None
@@ -175,7 +182,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
