@@ -700,3 +700,26 @@ def test_random_scene_parity(gpu_available, seed):
     blob, cam = _random_scene(seed)
     acc_g, acc_o, st = _compare(blob, cam)
     assert np.isfinite(acc_g).any() and acc_g[np.isfinite(acc_g)].mean() > 0.0
+
+
+@pytest.mark.parametrize("case", ["empty_world", "1x1_1spp_depth1", "1x1_4spp", "3x3_1spp",
+                                  "odd_17x11"])
+def test_degenerate_sizes_parity(gpu_available, case):
+    """Edge sizes of render.rs's loop: an empty world (every sample is the background,
+    render.rs:270-272), a one-pixel image (image_height >= 1, render.rs:70-71), one sample per
+    pixel (sqrt_spp = 1, render.rs:75-76), depth 1, and an odd size that fills no 8x8 tile."""
+    sc = rt.Scene(2)
+    world = (sc.hittable_list() if case == "empty_world" else
+             sc.hittable_list(sc.sphere((0, 0, 0), 0.5, sc.lambertian((0.5, 0.5, 0.5))),
+                              sc.quad((-2, -0.5, -2), (4, 0, 0), (0, 0, 4), sc.metal((0.8, 0.8, 0.8), 0.1))))
+    blob = sc.serialize(world)
+    wd, spp, depth, aspect = {"empty_world": (17, 4, 5, 1.5), "1x1_1spp_depth1": (1, 1, 1, 1.0),
+                              "1x1_4spp": (1, 4, 2, 1.0), "3x3_1spp": (3, 1, 50, 1.0),
+                              "odd_17x11": (17, 9, 10, 1.5)}[case]
+    cam = rt.camera_new(aspect, wd, spp, depth, 50, (0, 0.3, -3), (0, 0, 0), (0, 1, 0), 0, 0,
+                        (0.7, 0.8, 1.0))
+    acc_g, acc_o, st = _compare(blob, cam)
+    assert acc_g.shape == (cam.image_height, wd, 3)
+    if case == "empty_world":
+        n = cam.samples_per_pixel
+        assert np.allclose(acc_g, np.array([0.7, 0.8, 1.0], np.float32) * n, rtol=1e-6)
