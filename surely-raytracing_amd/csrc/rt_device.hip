@@ -464,22 +464,15 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   P.cbvh_bytes = sc->hdr.cbvh_words * 4u;
   P.cbvh_lds_off = ~0u;
   P.stack_lds_off = 0;
-  P.hint_lds_off = ~0u;
   size_t cbvh_lds = 0;
   {
     const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
-    const size_t stack = (size_t)RTL_CBVH_STACK * block * 2, hints = stack / 2;
-    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + stack;
+    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + (size_t)RTL_CBVH_STACK * block * 2;
     if (bvh && !count && P.cbvh_bytes && !(opts->flags & RT_FLAG_REFERENCE_BVH) &&
         !std::getenv("RT_NO_CBVH_LDS") && need <= cap) {
       P.cbvh_lds_off = P.stage_bytes;
       P.stack_lds_off = P.stage_bytes + P.cbvh_bytes;
       cbvh_lds = need - P.stage_bytes;
-      // the stack entries' u8 entry hints (cbvh_walk), where they fit too
-      if (need + hints <= cap && !std::getenv("RT_NO_CBVH_HINTS")) {
-        P.hint_lds_off = (uint32_t)need;
-        cbvh_lds += hints;
-      }
     }
   }
   if (P.stage_scene) {

@@ -307,10 +307,9 @@ struct TraceParams {
   uint32_t bvh_words, bvh_lds_words, bvh_lds_off;
   // compact ordered BVHs (rt_layout.h CBVH) staged in LDS for cbvh_walk: cbvh_bytes from
   // cbvh_src at LDS byte offset cbvh_lds_off (~0u: not staged, the OBVH streams are walked from
-  // global memory), the walk's per-lane u16 stacks at stack_lds_off and, when the workgroup's
-  // LDS has room, one u8 entry-time hint per stack entry at hint_lds_off (~0u: none)
+  // global memory), and the walk's per-lane u16 stacks at stack_lds_off
   const uint8_t* cbvh_src;
-  uint32_t cbvh_bytes, cbvh_lds_off, stack_lds_off, hint_lds_off;
+  uint32_t cbvh_bytes, cbvh_lds_off, stack_lds_off;
   uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
@@ -1319,18 +1318,6 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   const lw_t leaves = refs + n_int;
   const ls_t stack = reinterpret_cast<ls_t>((lbw_t)rt_lds + P.stack_lds_off) + threadIdx.x;
   const uint32_t sstride = blockDim.x;
-  // Entry hints: with each pushed child, a lower bound of its box's entry time tn (f32 bits of a
-  // positive tn >> 20, offset to 2^-10, so 3 mantissa bits; 0 means 0). A popped entry whose
-  // bound fails the box test against the current close_f is dropped: its own box test (a leaf's,
-  // as obvh_walk would make it) and every box below it would fail too, since a child's entry is
-  // never below its parent's and the test is monotone in tn (the f32 bounds grow outwards).
-  const bool hints = P.hint_lds_off != ~0u;
-  const lbw_t hint = (lbw_t)rt_lds + (hints ? P.hint_lds_off : 0u) + threadIdx.x;
-  constexpr int kHintBase = (127 - 10) << 3;
-  auto enc = [&](float t) -> uint32_t {
-    const int q = (int)(__float_as_uint(t) >> 20) - kHintBase;
-    return t > 0.0f ? (uint32_t)min(max(q, 0), 255) : 0u;
-  };
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
@@ -1368,18 +1355,6 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   constexpr uint32_t kDone = 0xffffu;
   uint32_t ref = hd.z & 0xffffu;
   uint32_t sp = 0;
-  // the next stacked entry whose hint passes (kDone when the stack runs out)
-  auto pop = [&]() -> uint32_t {
-    const float hi = fmaf(fabsf(close_f), kBoxRel, close_f);
-    while (sp > 0) {
-      --sp;
-      if (!hints) return stack[sp * sstride];
-      const uint32_t q = hint[sp * sstride];
-      const float lb = q ? __uint_as_float((q + kHintBase) << 20) : 0.0f;
-      if (fmaf(-lb, kBoxRel, lb) <= hi) return stack[sp * sstride];
-    }
-    return kDone;
-  };
   for (;;) {
     // while-while: steps until the lane holds a leaf whose box was hit (or is done), then the
     // leaves with every lane that has one. (Postponing a lane's leaf and stepping on until every
@@ -1397,20 +1372,27 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
       const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
       if (h0 & h1) {
         stack[sp * sstride] = (uint16_t)(first0 ? r1 : r0);
-        if (hints) hint[sp * sstride] = (uint8_t)enc(first0 ? tn1 : tn0);
         ++sp;
       }
       if (h0 | h1) {
         ref = first0 ? r0 : r1;
+      } else if (sp > 0) {
+        --sp;
+        ref = stack[sp * sstride];
       } else {
-        ref = pop();
+        ref = kDone;
       }
     }
     if (ref == kDone) break;
     const double closest_before = closest;
     obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin, cand);
     if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
-    ref = pop();
+    if (sp > 0) {
+      --sp;
+      ref = stack[sp * sstride];
+    } else {
+      ref = kDone;
+    }
   }
   flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
          (hit & (closest <= tmin * (1.0 + kTieRel)));
