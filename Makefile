@@ -81,3 +81,8 @@ variants-jocc: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=3 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w3.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=5 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w5.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=6 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w6.so -lhiprtc
+
+# cost probe of reference-order arithmetic (unfused products, IEEE division/sqrt); not shipped
+variants-exact: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_exact
+	$(HIPCC) $(HIPFLAGS) -DRT_EXACT_PROBE -shared $(DEV_SRC) -o $(BUILD)/variants_exact/librtmi355x_exact.so -lhiprtc

@@ -77,6 +77,30 @@ def parse():
     return a
 
 
+def host_parallelism():
+    """The reference's thread count: rayon's global pool uses std::thread::available_parallelism()
+    (render.rs:153-160), i.e. the CPUs this process may run on (sched_getaffinity), lowered to a
+    cgroup v2 CPU quota when one is set (cpu.max). Returns (threads, how it was determined)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+        how = f"sched_getaffinity: {n}"
+    except AttributeError:
+        n = os.cpu_count() or 1
+        how = f"os.cpu_count: {n}"
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            q = max(1, -(-int(quota) // int(period)))
+            how += f", cgroup cpu.max quota {quota}/{period} -> {q}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    if n > 512:  # the GPU box's process guard counts tasks (1024 at once); never expected here
+        how += f", capped at 512 of {n}"
+        n = 512
+    return max(1, n), how
+
+
 def cpu_baseline(blob, cam, seed, target_s):
     """f64 CPU oracle on a bounded sample of the same frame: full image, a subset of the
     sqrt_spp stratum rows (each sample keeps the full-spp jitter), 3-row chunks over a thread
@@ -85,11 +109,7 @@ def cpu_baseline(blob, cam, seed, target_s):
     import oracle_lib as O
     import surely_rt as rt
 
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(16, threads))
+    threads, how = host_parallelism()
     done_samples, elapsed, sj = 0, 0.0, 0
     S = cam.sqrt_spp
     while sj < S and elapsed < target_s:
@@ -106,7 +126,8 @@ def cpu_baseline(blob, cam, seed, target_s):
         "kind": "port",
         "sample": (f"{sj} of {S} stratum rows (s_j) over the full {cam.image_width}x"
                    f"{cam.image_height} frame = {done_samples} samples in {elapsed:.1f} s; "
-                   "f64 C restatement of the reference (oracle/rt_oracle.c), 3-row chunks"),
+                   "f64 C restatement of the reference (oracle/rt_oracle.c), 3-row chunks, one "
+                   f"thread per available core as rayon's pool ({how})"),
     }
 
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define RT_OK 0
@@ -233,7 +233,9 @@ int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
               rt_stats* stats);
 
 /* Asynchronous on `hip_stream` (hipStream_t, may be NULL): render into a DEVICE buffer.
- * If stats != NULL the call synchronises the stream to fill it. */
+ * If stats != NULL the call synchronises the stream to fill it. Limits: image_width <= 65535
+ * (RT_ERR_UNSUPPORTED beyond); any number of rows (row ranges taller than 32760 rows run as
+ * consecutive sub-renders, same image). rt_scene_destroy waits for the scene's renders. */
 int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
                      float* accum_rgb_device, void* hip_stream, rt_stats* stats);
 
@@ -258,6 +260,25 @@ int rt_scene_prof_counters(rt_scene* scene, uint64_t* out, int n);
  * gather. */
 int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,
                     const int* devices, int n_devices, float* accum_rgb, rt_stats* stats);
+
+/* Persistent multi-GPU handle (one host process driving N GPUs, frame after frame; the same
+ * role as render_par_lights rendering one frame per call over every core, render.rs:144-216).
+ * rt_multi_create uploads the scene to each listed device ONCE (a device may be listed more than
+ * once); every device keeps its scene, workspace, stream, row buffer and compiled kernel across
+ * calls. rt_multi_render: the call's rows are dealt cyclically (row r of the call -> devices[r mod
+ * n]), every device renders its rows on its own stream, the rows are copied peer to peer
+ * (hipMemcpyPeerAsync, xGMI) into a staging buffer on devices[0], and a kernel there
+ * de-interleaves them into accum_rgb_device0 (a devices[0] buffer of opts->n_rows * W * 3
+ * floats; overwritten or added to as opts->flags says). Asynchronous on hip_stream (a devices[0]
+ * stream, may be NULL); stats != NULL synchronises it. Bit for bit the image of rt_render_device
+ * on one device. rt_multi_info: out[0..3] = frames rendered, scene uploads, staging-buffer
+ * allocations, devices. */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const rt_scene_blob* blob, const int* devices, int n_devices, rt_multi** out);
+int rt_multi_render(rt_multi* multi, const rt_camera* cam, const rt_render_opts* opts,
+                    float* accum_rgb_device0, void* hip_stream, rt_stats* stats);
+int rt_multi_info(rt_multi* multi, uint64_t* out, int n);
+void rt_multi_destroy(rt_multi* multi);
 
 /* One-shot drop-in for render_par_lights: create + render + destroy. */
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,

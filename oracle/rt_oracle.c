@@ -178,6 +178,7 @@ static float f32_acos(float x) {
 
 #if ORACLE_F64
 #define LOG log
+#define POW pow /* f64::powf */
 #define SIN sin
 #define ACOS acos
 #define ATAN2 atan2
@@ -189,6 +190,7 @@ static void sincos2pi(double u, double* s, double* c) {
 #define INV_PI (1.0 / PI_D)
 #else
 #define LOG f32_log
+#define POW powf
 #define SIN f32_sin
 #define ACOS f32_acos
 #define ATAN2 f32_atan2
@@ -944,12 +946,9 @@ static vec3 ray_color(ctx_t* cx, const camctx* cc, const ray_t* r, int depth, rn
     int cannot = ratio * sin_t > R(1);
     int refl = cannot;
     if (!cannot) {
-      real r0 = (R(1) - ratio) / (R(1) + ratio);
+      real r0 = (R(1) - ratio) / (R(1) + ratio); /* Dielectric::reflectance material.rs:156-163 */
       r0 = r0 * r0;
-      real x = R(1) - cos_t;
-      real x2 = x * x;
-      real x5 = (x2 * x2) * x;
-      real reflectance = FMA(R(1) - r0, x5, r0);
+      real reflectance = r0 + (R(1) - r0) * POW(R(1) - cos_t, R(5));
       refl = reflectance > rnd(g);
     }
     vec3 dir = refl ? reflect(ud, rec.normal) : refract(ud, rec.normal, ratio);

@@ -132,6 +132,24 @@ __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part
   }
 }
 
+// rt_multi_render's gather on the first device: device k's compact rows (its cyclic share of
+// the call's rows, k, k + G, ...) arrive in `stage` at row offset row0[k]; each row goes to row
+// k + j * G of the frame, overwritten or added (the caller's accumulator, render.rs:189).
+__global__ __launch_bounds__(256) void rt_deinterleave(const float* __restrict__ stage,
+                                                       float* __restrict__ frame, int row_floats,
+                                                       int n_rows, int G, int overwrite) {
+  const int kr = blockIdx.y;  // row of the frame
+  if (kr >= n_rows) return;
+  const int k = kr % G, j = kr / G;
+  // device k's rows start at sum_{k' < k} rows(k'), rows(k') = ceil((n_rows - k') / G)
+  int row0 = 0;
+  for (int q = 0; q < k; ++q) row0 += (n_rows - q + G - 1) / G;
+  const float* src = stage + (size_t)(row0 + j) * row_floats;
+  float* dst = frame + (size_t)kr * row_floats;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
+    dst[i] = overwrite ? src[i] : dst[i] + src[i];
+}
+
 // ---------------------------------------------------------------- host side
 thread_local std::string g_err;
 
@@ -323,7 +341,13 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
 
 void rt_scene_destroy(rt_scene* sc) {
   if (!sc) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
   (void)hipSetDevice(sc->device);
+  // renders are asynchronous on the caller's streams (rt_render_device): wait for them before
+  // the module cache may unload this scene's kernel code object (release_kernel evicts idle
+  // modules) and before the tables and workspace are freed
+  (void)hipDeviceSynchronize();
   for (const rtj::Kernel& k : sc->jit_k) rtj::release_kernel(k);  // the module cache's holds
   if (sc->dev) (void)hipFree(sc->dev);
   if (sc->work) (void)hipFree(sc->work);
@@ -334,6 +358,7 @@ void rt_scene_destroy(rt_scene* sc) {
     for (int j = 0; j < 2; ++j)
       if (sc->tev[k][j]) (void)hipEventDestroy(sc->tev[k][j]);
   delete sc;
+  if (prev >= 0) (void)hipSetDevice(prev);
 }
 
 uint64_t rt_scene_device_bytes(const rt_scene* sc) { return sc ? sc->dev_bytes : 0; }
@@ -376,8 +401,8 @@ int rt_scene_jit_info(rt_scene* sc, int* state, char* msg, uint32_t msg_len) {
   return RT_OK;
 }
 
-int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
-                     float* accum, void* stream_v, rt_stats* stats) {
+static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
+                              float* accum, void* stream_v, rt_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!sc || !cam || !opts || !accum) return set_err(RT_ERR_INVALID_ARG, "null argument");
   const int W = cam->image_width, S = cam->sqrt_spp;
@@ -721,6 +746,41 @@ int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* o
   return RT_OK;
 }
 
+// Lane item keys hold the call's row index in 15 bits (render_device_rows): taller row ranges
+// are rendered as consecutive sub-calls of kRowsPerCall rows into the matching rows of accum.
+// The RNG is keyed by the global pixel and sample, so the image does not depend on the split.
+constexpr int kRowsPerCall = 32760;
+
+int rt_render_device(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
+                     float* accum, void* stream_v, rt_stats* stats) {
+  if (!sc || !cam || !opts || !accum) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  if (opts->n_rows <= kRowsPerCall || cam->image_width <= 0)
+    return render_device_rows(sc, cam, opts, accum, stream_v, stats);
+  auto t0 = std::chrono::steady_clock::now();
+  rt_stats part{}, sum{};
+  for (int k0 = 0; k0 < opts->n_rows; k0 += kRowsPerCall) {
+    rt_render_opts o = *opts;
+    o.row_begin = opts->row_begin + k0 * opts->row_step;
+    o.n_rows = std::min(kRowsPerCall, opts->n_rows - k0);
+    const int rc = render_device_rows(sc, cam, &o, accum + (size_t)k0 * cam->image_width * 3,
+                                      stream_v, stats ? &part : nullptr);
+    if (rc != RT_OK) return rc;
+    if (stats) {
+      sum.ms_kernel += part.ms_kernel;
+      sum.samples += part.samples;
+      sum.out_bytes += part.out_bytes;
+      sum.launches += part.launches;
+      for (int k = 0; k < 32; ++k) sum.ops[k] += part.ops[k];
+    }
+  }
+  if (stats) {
+    sum.ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *stats = sum;
+  }
+  return RT_OK;
+}
+
 // Profiling builds (-DRT_PROF, not shipped): the ordered-BVH walk counters of the last render
 // (rt_kernel.h obvh_walk). Other builds return zeros.
 int rt_scene_prof_counters(rt_scene* sc, uint64_t* out, int n) {
@@ -798,6 +858,8 @@ int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_re
     return set_err(RT_ERR_INVALID_ARG, "bad row range");
   const int W = cam->image_width, G = n_devices;
   const size_t row_floats = (size_t)W * 3;
+  int prev_device = -1;  // the caller's current device, restored on return
+  (void)hipGetDevice(&prev_device);
   struct Part {
     rt_scene* sc = nullptr;
     hipStream_t stream = nullptr;
@@ -873,7 +935,208 @@ int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_re
   const std::string err = rc == RT_OK ? std::string() : g_err;
   cleanup();
   if (rc != RT_OK) g_err = err;
+  if (prev_device >= 0) (void)hipSetDevice(prev_device);
   return rc;
+}
+
+// ---------------------------------------------------------------- persistent multi-GPU handle
+// rt_multi_create uploads the scene to every listed device once; each device keeps its scene,
+// its workspace, its stream, its compact row buffer and (after the first frame) its compiled
+// scene-specialised kernel across rt_multi_render calls. A frame: every device renders its
+// cyclic rows into its own buffer on its own stream, the buffers are copied peer-to-peer
+// (hipMemcpyPeerAsync: xGMI between MI355X devices) into a staging area on the first device,
+// and one kernel there de-interleaves the rows into the caller's frame.
+struct rt_multi {
+  struct Dev {
+    rt_scene* sc = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    float* rows = nullptr;  // compact rows of this device's share
+    size_t rows_bytes = 0;
+  };
+  std::vector<int> devices;
+  std::vector<Dev> dev;
+  float* stage = nullptr;  // on devices[0]: every device's rows, device after device
+  size_t stage_bytes = 0;
+  hipEvent_t start = nullptr;  // on devices[0]: the frame's start on the caller's stream
+  uint64_t frames = 0, uploads = 0, stage_allocs = 0;
+  std::mutex mu;
+};
+
+int rt_multi_create(const rt_scene_blob* blob, const int* devices, int n_devices,
+                    rt_multi** out) {
+  if (!blob || !devices || n_devices <= 0 || !out)
+    return set_err(RT_ERR_INVALID_ARG, "null argument or no devices");
+  *out = nullptr;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  rt_multi* m = new rt_multi();
+  m->devices.assign(devices, devices + n_devices);
+  m->dev.resize(n_devices);
+  int rc = RT_OK;
+  for (int k = 0; k < n_devices && rc == RT_OK; ++k) {
+    rc = rt_scene_create(blob, devices[k], &m->dev[k].sc);
+    if (rc != RT_OK) break;
+    ++m->uploads;
+    hipError_t e = hipStreamCreateWithFlags(&m->dev[k].stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&m->dev[k].done, hipEventDisableTiming);
+    // direct peer copies into the first device (already enabled / same device: not an error)
+    if (e == hipSuccess && devices[k] != devices[0]) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[k], devices[0]) == hipSuccess && can) {
+        const hipError_t pe = hipDeviceEnablePeerAccess(devices[0], 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) e = pe;
+        (void)hipGetLastError();
+      }
+    }
+    if (e != hipSuccess) rc = set_err(RT_ERR_HIP, std::string("rt_multi_create: ") + hipGetErrorString(e));
+  }
+  if (rc == RT_OK) {
+    hipError_t e = hipSetDevice(devices[0]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&m->start, hipEventDisableTiming);
+    if (e != hipSuccess) rc = set_err(RT_ERR_HIP, std::string("rt_multi_create: ") + hipGetErrorString(e));
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (rc != RT_OK) {
+    const std::string err = g_err;
+    rt_multi_destroy(m);
+    g_err = err;
+    return rc;
+  }
+  *out = m;
+  return RT_OK;
+}
+
+void rt_multi_destroy(rt_multi* m) {
+  if (!m) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (size_t k = 0; k < m->dev.size(); ++k) {
+    rt_multi::Dev& d = m->dev[k];
+    (void)hipSetDevice(m->devices[k]);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    if (d.rows) (void)hipFree(d.rows);
+    if (d.done) (void)hipEventDestroy(d.done);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    rt_scene_destroy(d.sc);
+  }
+  (void)hipSetDevice(m->devices[0]);
+  if (m->stage) (void)hipFree(m->stage);
+  if (m->start) (void)hipEventDestroy(m->start);
+  delete m;
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opts,
+                    float* accum_rgb_device0, void* hip_stream, rt_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!m || !cam || !opts || !accum_rgb_device0)
+    return set_err(RT_ERR_INVALID_ARG, "null argument");
+  if (opts->n_rows < 0 || opts->row_step <= 0 || cam->image_width <= 0)
+    return set_err(RT_ERR_INVALID_ARG, "bad row range");
+  if (opts->n_rows > 0 &&
+      (int64_t)opts->row_begin + (int64_t)(opts->n_rows - 1) * opts->row_step >= cam->image_height)
+    return set_err(RT_ERR_INVALID_ARG, "row range outside the image");
+  std::lock_guard<std::mutex> lock(m->mu);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  const int G = (int)m->devices.size(), d0 = m->devices[0];
+  const size_t row_floats = (size_t)cam->image_width * 3;
+  const size_t frame_bytes = (size_t)opts->n_rows * row_floats * sizeof(float);
+  hipStream_t out_stream = (hipStream_t)hip_stream;
+  auto fail = [&](hipError_t e, const char* what) {
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return set_err(RT_ERR_HIP, std::string("rt_multi_render ") + what + ": " + hipGetErrorString(e));
+  };
+  if (opts->n_rows == 0) return RT_OK;
+  hipError_t e = hipSetDevice(d0);
+  if (e == hipSuccess && m->stage_bytes < frame_bytes) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    e = hipMalloc(&m->stage, frame_bytes);
+    if (e == hipSuccess) m->stage_bytes = frame_bytes, ++m->stage_allocs;
+  }
+  if (e != hipSuccess) return fail(e, "staging buffer");
+  // the caller's stream on the first device orders the frame: every device starts after it
+  e = hipEventRecord(m->start, out_stream);
+  if (e != hipSuccess) return fail(e, "start event");
+  std::vector<char> used(G, 0);
+  uint64_t samples = 0;
+  size_t row0 = 0;
+  int rc = RT_OK;
+  for (int k = 0; k < G && rc == RT_OK; ++k) {
+    rt_multi::Dev& d = m->dev[k];
+    rt_render_opts o = *opts;
+    o.row_begin = opts->row_begin + k * opts->row_step;
+    o.row_step = opts->row_step * G;
+    o.n_rows = k < opts->n_rows ? (opts->n_rows - k + G - 1) / G : 0;
+    o.device = m->devices[k];
+    o.flags |= RT_FLAG_OVERWRITE;  // compact rows; the gather applies the caller's mode
+    if (o.n_rows == 0) continue;
+    const size_t bytes = (size_t)o.n_rows * row_floats * sizeof(float);
+    e = hipSetDevice(m->devices[k]);
+    if (e == hipSuccess && d.rows_bytes < bytes) {
+      if (d.rows) (void)hipFree(d.rows);
+      d.rows = nullptr;
+      d.rows_bytes = 0;
+      e = hipMalloc(&d.rows, bytes);
+      if (e == hipSuccess) d.rows_bytes = bytes;
+    }
+    if (e == hipSuccess) e = hipStreamWaitEvent(d.stream, m->start, 0);
+    if (e != hipSuccess) {
+      rc = fail(e, "device setup");
+      break;
+    }
+    rc = rt_render_device(d.sc, cam, &o, d.rows, d.stream, nullptr);
+    if (rc != RT_OK) break;
+    // the rows travel to the first device's staging area (xGMI peer copy, or a local copy)
+    e = hipMemcpyPeerAsync(m->stage + row0 * row_floats, d0, d.rows, m->devices[k], bytes, d.stream);
+    if (e == hipSuccess) e = hipEventRecord(d.done, d.stream);
+    if (e != hipSuccess) {
+      rc = fail(e, "peer copy");
+      break;
+    }
+    used[k] = 1;
+    samples += (uint64_t)o.n_rows * cam->image_width *
+               (uint64_t)(opts->sj_count > 0 ? opts->sj_count : cam->sqrt_spp) * cam->sqrt_spp;
+    row0 += (size_t)o.n_rows;
+  }
+  if (rc == RT_OK) {
+    e = hipSetDevice(d0);
+    for (int k = 0; k < G && e == hipSuccess; ++k)
+      if (used[k]) e = hipStreamWaitEvent(out_stream, m->dev[k].done, 0);
+    if (e == hipSuccess) {
+      const int gx = (int)std::min<size_t>(64, (row_floats + 255) / 256);
+      hipLaunchKernelGGL(rt_deinterleave, dim3((unsigned)gx, (unsigned)opts->n_rows), dim3(256), 0,
+                         out_stream, m->stage, accum_rgb_device0, (int)row_floats, opts->n_rows, G,
+                         (opts->flags & RT_FLAG_OVERWRITE) ? 1 : 0);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess && stats) e = hipStreamSynchronize(out_stream);
+    if (e != hipSuccess) rc = fail(e, "gather");
+  }
+  if (rc == RT_OK) {
+    ++m->frames;
+    if (stats) {
+      std::memset(stats, 0, sizeof(*stats));
+      stats->samples = samples;
+      stats->launches = (uint32_t)G;
+      stats->ms_total =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      stats->ms_kernel = stats->ms_total;
+    }
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return rc;
+}
+
+int rt_multi_info(rt_multi* m, uint64_t* out, int n) {
+  if (!m || !out || n < 0) return set_err(RT_ERR_INVALID_ARG, "null argument");
+  std::lock_guard<std::mutex> lock(m->mu);
+  const uint64_t v[4] = {m->frames, m->uploads, m->stage_allocs, (uint64_t)m->devices.size()};
+  for (int k = 0; k < n && k < 4; ++k) out[k] = v[k];
+  return RT_OK;
 }
 
 int rt_render_blob(const rt_scene_blob* blob, const rt_camera* cam, const rt_render_opts* opts,

@@ -78,6 +78,10 @@ struct MinWaves {
 struct d3 {
   double x, y, z;
 };
+#ifdef RT_EXACT_PROBE  // cost probe (not shipped): unfused products, IEEE division and sqrt
+__device__ __forceinline__ double rt_unfused_fma(double a, double b, double c) { return a * b + c; }
+#define fma(a, b, c) rt_unfused_fma(a, b, c)
+#endif
 __device__ __forceinline__ d3 mk(double x, double y, double z) { return {x, y, z}; }
 __device__ __forceinline__ d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
@@ -105,6 +109,14 @@ __device__ __forceinline__ d3 cross(d3 u, d3 v) {  // vec3.rs:171-177
 // sequences). Used only where the operand is finite and non-zero by construction (quad
 // denominators past the 1e-8 test, |d|^2, |v|^2 of non-degenerate vectors); radiance weights
 // keep IEEE division so 0/0 stays NaN exactly as in the reference.
+#ifdef RT_EXACT_PROBE
+__device__ __forceinline__ double rcp_nr(double b) { return 1.0 / b; }
+__device__ __forceinline__ double rcp_nr1(double b) { return 1.0 / b; }
+__device__ __forceinline__ double div_nr(double a, double b) { return a / b; }
+__device__ __forceinline__ double rsq_nr(double x) { return 1.0 / __builtin_sqrt(x); }
+__device__ __forceinline__ double rcp_w(double b) { return 1.0 / b; }
+__device__ __forceinline__ double sqrt_nr(double x) { return __builtin_sqrt(x); }
+#else
 __device__ __forceinline__ double rcp_nr(double b) {
   double r = __builtin_amdgcn_rcp(b);
   r = fma(fma(-b, r, 1.0), r, r);
@@ -155,6 +167,7 @@ __device__ __forceinline__ double sqrt_nr(double x) {
   s = fma(e, h, s);
   return __builtin_amdgcn_class(x, 0x260) ? x : s;  // +-0, +inf
 }
+#endif
 __device__ __forceinline__ d3 unit_vector(d3 v) {  // vec3.rs:179-181
   return v * rsq_nr(dot(v, v));
 }
@@ -165,6 +178,17 @@ __device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-2
   double c = fmin(dot(-uv, n), 1.0);
   d3 perp = e * vfma(c, n, uv);
   return vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), n, perp);
+}
+
+// x^5 correctly rounded, for Schlick's (1 - cos)^5 (material.rs:162 calls powf(5.), i.e. the
+// platform pow). x^2 is formed exactly as a double-double (a + ae), squared and multiplied by x
+// in double-double (relative error ~2^-104), then rounded once: the IEEE-rounded x^5 except
+// for exact values within ~2^-104 of a rounding midpoint (dielectric bounces only).
+__device__ __forceinline__ double pow5_cr(double x) {
+  const double a = x * x, ae = fma(x, x, -a);
+  const double b = a * a, be = fma(a, a, -b) + (2.0 * a) * ae;
+  const double c = b * x, ce = fma(b, x, -c) + be * x;
+  return c + ce;
 }
 
 // An f64 constant materialised at its point of use: two s_mov_b32 into an SGPR pair, which the
@@ -2150,9 +2174,9 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     double u0 = 0.0;
     if (diel ? !tir : have_lights) u0 = rnd(g);
     const double r0s = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
-    const double xx = 1.0 - cos_t;
-    const double x2 = xx * xx;
-    const bool refl = tir || fma(1.0 - r0s, x2 * x2 * xx, r0s) > u0;
+    // reflectance r0 + (1 - r0) * (1 - cos)^5 in the reference's operation order (material.rs:
+    // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr)
+    const bool refl = tir || r0s + (1.0 - r0s) * pow5_cr(1.0 - cos_t) > u0;
     const bool light_branch = !diel && have_lights && u0 < 0.5;
     d3 dir = mk(0., 0., 0.), factor = mk(0., 0., 0.);
     double cos_sl = cos_sl0;

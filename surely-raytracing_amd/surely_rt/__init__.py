@@ -195,6 +195,12 @@ def load_device_lib(path: Path) -> C.CDLL:
         "rt_scene_trace_ms": (C.c_int, [p, C.POINTER(C.c_float), C.c_int,
                                         C.POINTER(C.c_int)]),
         "rt_scene_jit_info": (C.c_int, [p, C.POINTER(C.c_int), C.c_char_p, C.c_uint32]),
+        "rt_multi_create": (C.c_int, [C.POINTER(RtSceneBlob), C.POINTER(C.c_int), C.c_int,
+                                      C.POINTER(p)]),
+        "rt_multi_render": (C.c_int, [p, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
+                                      C.c_void_p, C.POINTER(RtStats)]),
+        "rt_multi_info": (C.c_int, [p, C.POINTER(C.c_uint64), C.c_int]),
+        "rt_multi_destroy": (None, [p]),
         "rt_jit_check": (C.c_int, [C.POINTER(RtSceneBlob), C.c_char_p, C.POINTER(C.c_int),
                                    C.c_char_p, C.c_uint32]),
     }
@@ -202,7 +208,7 @@ def load_device_lib(path: Path) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rt_abi_version() != 2:
+    if lib.rt_abi_version() != 3:
         raise RuntimeError("librtmi355x ABI version mismatch")
     return lib
 
@@ -504,6 +510,42 @@ def render_multi(blob: "Blob", cam: RtCamera, opts: RtRenderOpts, devices,
     _check_dev(device_lib().rt_render_multi(blob.ref(), C.byref(cam), C.byref(opts), devs,
                                             len(devices), accum.ctypes.data, C.byref(st)))
     return accum, st
+
+
+class MultiScene:
+    """rt_multi_*: the scene resident on several GPUs of one process, frame after frame; rows are
+    dealt cyclically and gathered peer to peer into a buffer on devices[0]."""
+
+    def __init__(self, blob: "Blob", devices):
+        self._lib = device_lib()
+        self._blob = blob
+        self.devices = list(devices)
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        _check_dev(self._lib.rt_multi_create(blob.ref(), devs, len(self.devices), C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def render_device(self, cam: RtCamera, opts: RtRenderOpts, dev_ptr: int, stream: int = 0,
+                      stats: bool = False):
+        """Asynchronous frame into a devices[0] buffer (e.g. a torch tensor's data_ptr())."""
+        st = RtStats() if stats else None
+        _check_dev(self._lib.rt_multi_render(self._h, C.byref(cam), C.byref(opts),
+                                             C.c_void_p(dev_ptr), C.c_void_p(stream or None),
+                                             C.byref(st) if st is not None else None))
+        return st
+
+    def info(self) -> dict:
+        out = (C.c_uint64 * 4)()
+        _check_dev(self._lib.rt_multi_info(self._h, out, 4))
+        return dict(zip(("frames", "uploads", "stage_allocs", "devices"), (int(v) for v in out)))
 
 
 def validate(blob: "Blob") -> int:

@@ -60,7 +60,11 @@ def render(blob, cam: RtCamera, opts: RtRenderOpts, precision: int = 64, threads
            accum: np.ndarray | None = None):
     """oracle_render -> (accum float32 [n_rows, W, 3], op-count dict)."""
     if threads is None:
-        threads = min(8, os.cpu_count() or 1)
+        try:
+            threads = len(os.sched_getaffinity(0))
+        except AttributeError:
+            threads = os.cpu_count() or 1
+        threads = max(1, min(16, threads))  # the GPU box's CPU share is 16 (8 here)
     shape = (opts.n_rows, cam.image_width, 3)
     if accum is None:
         accum = np.zeros(shape, np.float32)

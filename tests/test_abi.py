@@ -30,7 +30,7 @@ def test_exports_every_declared_symbol(header, lib):
 
 def test_abi_version_and_error_string():
     lib = rt.device_lib()
-    assert lib.rt_abi_version() == 2
+    assert lib.rt_abi_version() == 3
     assert isinstance(lib.rt_last_error(), bytes)
 
 
