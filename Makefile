@@ -24,7 +24,7 @@ all: device host oracle cli
 device: $(BUILD)/librtmi355x.so
 host: $(BUILD)/librthost.so
 cli: $(BUILD)/rt_render_cli
-oracle: oracle/_build/liboracle_f32.so oracle/_build/liboracle_f64.so
+oracle: oracle/_build/liboracle_f32.so oracle/_build/liboracle_f64.so oracle/_build/liboracle_f64fma.so
 
 # device headers embedded for the scene-specialised kernels compiled at run time (rt_jit.cpp)
 $(BUILD)/rt_jit_sources.inc: $(JIT_HDR) $(CSRC)/embed_sources.py
@@ -49,6 +49,11 @@ oracle/_build/liboracle_f32.so: oracle/rt_oracle.c include/rt_mi355x.h
 oracle/_build/liboracle_f64.so: oracle/rt_oracle.c include/rt_mi355x.h
 	@mkdir -p oracle/_build
 	gcc $(CFLAGS_O) -DORACLE_F64=1 -shared $< -o $@ -lpthread -lm
+
+# perturbation study (tools/flip_study.py): the f64 oracle with fused dot products
+oracle/_build/liboracle_f64fma.so: oracle/rt_oracle.c include/rt_mi355x.h
+	@mkdir -p oracle/_build
+	gcc $(CFLAGS_O) -DORACLE_F64=1 -DORACLE_FMA_DOT=1 -shared $< -o $@ -lpthread -lm
 
 clean:
 	rm -rf $(BUILD) oracle/_build
@@ -81,6 +86,11 @@ variants-jocc: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=3 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w3.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=5 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w5.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=6 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w6.so -lhiprtc
+
+# A/B of the compact-BVH walk's step loop: the round-2 branching form
+variants-cbvh: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_cbvh
+	$(HIPCC) $(HIPFLAGS) -DRT_CBVH_BRANCHY -shared $(DEV_SRC) -o $(BUILD)/variants_cbvh/librtmi355x_branchy.so -lhiprtc
 
 # cost probe of reference-order arithmetic (unfused products, IEEE division/sqrt); not shipped
 variants-exact: $(DEV_SRC) $(DEV_HDR)

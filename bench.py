@@ -185,7 +185,7 @@ def main():
         ops = st.op_counts()
 
     # one product render with stats (outside the timed region): the bytes the path kernel
-    # stores per launch (f64 row partials + tail samples) = its algorithmic HBM bytes
+    # stores per launch (f64 segment partials + tail samples: its workspace)
     pst = ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream, stats=True)
     out_bytes_launch = pst.out_bytes / max(1, pst.launches)
     for _ in range(args.warmup):
@@ -256,6 +256,13 @@ def main():
                     prof = json.loads(tf.read_text())
                 except Exception:
                     prof = None
+            # a profile of another kernel build is stale: its bytes are not this kernel's
+            stale = None
+            if prof and prof.get("kernel_source_sha16") != roofline.kernel_source_sha16():
+                stale = (f"profiles/{tf.name} was collected on kernel sources "
+                         f"{prof.get('kernel_source_sha16')}, this tree is "
+                         f"{roofline.kernel_source_sha16()}: traffic not reported")
+                prof = None
             traffic = prof.get("hbm_bytes_per_launch") if prof else None
             res["roofline"] = {
                 "bound": "valu", "achieved": round(ach, 3),
@@ -270,8 +277,17 @@ def main():
                 "render_ms": round(step_gpu_ms, 3),
                 "flops_per_launch": fl / max(1, pst.launches),
                 "flops_per_sample": round(fl / ops["samples"], 1),
-                "algorithmic_bytes_per_launch": out_bytes_launch,
+                # the path's only mandatory HBM traffic is the framebuffer, W*H*12 B
+                # of f32 RGB per frame (written by rt_reduce). rt_trace's own stores are the f64
+                # partial-sum workspace, a design choice reported separately.
+                "algorithmic_bytes_per_frame": W * n * 12,
+                "workspace_bytes_per_launch": out_bytes_launch,
             }
+            if stale:
+                res["roofline"]["traffic_note"] = stale
+            if traffic is not None:
+                res["roofline"]["traffic_per_algorithmic_byte"] = round(
+                    traffic * pst.launches / (W * n * 12), 1)
             if traffic is not None:
                 launch_s = kernel_ms * 1e-3 / max(1, pst.launches)
                 res["hbm"] = {

@@ -258,9 +258,14 @@ static inline vec3 vscale(vec3 a, real t) { return v3(a.x * t, a.y * t, a.z * t)
 static inline vec3 vfma(real t, vec3 a, vec3 b) { /* t*a + b */
   return v3(FMA(t, a.x, b.x), FMA(t, a.y, b.y), FMA(t, a.z, b.z));
 }
-#if ORACLE_F64
+#if ORACLE_F64 && !ORACLE_FMA_DOT
 /* vec3.rs:167-169 / 74-76: (x*x' + y*y') + z*z', evaluated left to right */
 static inline real dot(vec3 a, vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+#elif ORACLE_F64
+/* perturbation study only (liboracle_f64fma.so, tools/flip_study.py): the dot product fused as
+ * the device evaluates it, every other operation as above. Differs from the reference order in
+ * the last bits of each dot product; the study measures how often that alone changes a path. */
+static inline real dot(vec3 a, vec3 b) { return fma(a.x, b.x, fma(a.y, b.y, a.z * b.z)); }
 #else
 static inline real dot(vec3 a, vec3 b) { return FMA(a.x, b.x, FMA(a.y, b.y, a.z * b.z)); }
 #endif

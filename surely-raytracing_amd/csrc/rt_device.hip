@@ -135,19 +135,25 @@ __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part
 // rt_multi_render's gather on the first device: device k's compact rows (its cyclic share of
 // the call's rows, k, k + G, ...) arrive in `stage` at row offset row0[k]; each row goes to row
 // k + j * G of the frame, overwritten or added (the caller's accumulator, render.rs:189).
-__global__ __launch_bounds__(256) void rt_deinterleave(const float* __restrict__ stage,
+// to_frame = 0: the reverse (the caller's accumulator rows into the staging area, so that every
+// device accumulates into its own rows exactly as rt_render_device does, render.rs:189).
+__global__ __launch_bounds__(256) void rt_deinterleave(float* __restrict__ stage,
                                                        float* __restrict__ frame, int row_floats,
-                                                       int n_rows, int G, int overwrite) {
+                                                       int n_rows, int G, int to_frame) {
   const int kr = blockIdx.y;  // row of the frame
   if (kr >= n_rows) return;
   const int k = kr % G, j = kr / G;
   // device k's rows start at sum_{k' < k} rows(k'), rows(k') = ceil((n_rows - k') / G)
   int row0 = 0;
   for (int q = 0; q < k; ++q) row0 += (n_rows - q + G - 1) / G;
-  const float* src = stage + (size_t)(row0 + j) * row_floats;
-  float* dst = frame + (size_t)kr * row_floats;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
-    dst[i] = overwrite ? src[i] : dst[i] + src[i];
+  float* st = stage + (size_t)(row0 + j) * row_floats;
+  float* fr = frame + (size_t)kr * row_floats;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x) {
+    if (to_frame)
+      fr[i] = st[i];
+    else
+      st[i] = fr[i];
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -1058,6 +1064,14 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
     if (e == hipSuccess) m->stage_bytes = frame_bytes, ++m->stage_allocs;
   }
   if (e != hipSuccess) return fail(e, "staging buffer");
+  const bool accumulate = !(opts->flags & RT_FLAG_OVERWRITE);
+  const int gx = (int)std::min<size_t>(64, (row_floats + 255) / 256);
+  if (accumulate) {  // the caller's rows to the staging area: each device accumulates its own
+    hipLaunchKernelGGL(rt_deinterleave, dim3((unsigned)gx, (unsigned)opts->n_rows), dim3(256), 0,
+                       out_stream, m->stage, accum_rgb_device0, (int)row_floats, opts->n_rows, G, 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(e, "scatter");
+  }
   // the caller's stream on the first device orders the frame: every device starts after it
   e = hipEventRecord(m->start, out_stream);
   if (e != hipSuccess) return fail(e, "start event");
@@ -1072,7 +1086,7 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
     o.row_step = opts->row_step * G;
     o.n_rows = k < opts->n_rows ? (opts->n_rows - k + G - 1) / G : 0;
     o.device = m->devices[k];
-    o.flags |= RT_FLAG_OVERWRITE;  // compact rows; the gather applies the caller's mode
+    // compact rows: overwritten, or the caller's rows (scattered above) accumulated into
     if (o.n_rows == 0) continue;
     const size_t bytes = (size_t)o.n_rows * row_floats * sizeof(float);
     e = hipSetDevice(m->devices[k]);
@@ -1084,6 +1098,8 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
       if (e == hipSuccess) d.rows_bytes = bytes;
     }
     if (e == hipSuccess) e = hipStreamWaitEvent(d.stream, m->start, 0);
+    if (e == hipSuccess && accumulate)
+      e = hipMemcpyPeerAsync(d.rows, m->devices[k], m->stage + row0 * row_floats, d0, bytes, d.stream);
     if (e != hipSuccess) {
       rc = fail(e, "device setup");
       break;
@@ -1107,10 +1123,8 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
     for (int k = 0; k < G && e == hipSuccess; ++k)
       if (used[k]) e = hipStreamWaitEvent(out_stream, m->dev[k].done, 0);
     if (e == hipSuccess) {
-      const int gx = (int)std::min<size_t>(64, (row_floats + 255) / 256);
       hipLaunchKernelGGL(rt_deinterleave, dim3((unsigned)gx, (unsigned)opts->n_rows), dim3(256), 0,
-                         out_stream, m->stage, accum_rgb_device0, (int)row_floats, opts->n_rows, G,
-                         (opts->flags & RT_FLAG_OVERWRITE) ? 1 : 0);
+                         out_stream, m->stage, accum_rgb_device0, (int)row_floats, opts->n_rows, G, 1);
       e = hipGetLastError();
     }
     if (e == hipSuccess && stats) e = hipStreamSynchronize(out_stream);

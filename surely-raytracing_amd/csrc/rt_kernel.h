@@ -1331,7 +1331,6 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
                           int& hit_frame, bool& flag) {
   typedef const __attribute__((address_space(3))) uint8_t* lb_t;
-  typedef __attribute__((address_space(3))) uint16_t* ls_t;
   typedef __attribute__((address_space(3))) uint8_t* lbw_t;
   typedef const __attribute__((address_space(3))) uint32_t* lw_t;
   const gptr N = (gptr)P.nodes;
@@ -1340,8 +1339,15 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   const lu4ptr nodes = reinterpret_cast<lu4ptr>(base);
   const lw_t refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
   const lw_t leaves = refs + n_int;
+#ifdef RT_CBVH_BRANCHY
+  typedef __attribute__((address_space(3))) uint16_t* ls_t;
   const ls_t stack = reinterpret_cast<ls_t>((lbw_t)rt_lds + P.stack_lds_off) + threadIdx.x;
   const uint32_t sstride = blockDim.x;
+#else
+  // the lane's stack entries are blockDim.x u16 apart; sp is kept as a byte offset
+  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 2u * threadIdx.x;
+  const uint32_t sstep = 2u * blockDim.x;
+#endif
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
@@ -1379,6 +1385,11 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   constexpr uint32_t kDone = 0xffffu;
   uint32_t ref = hd.z & 0xffffu;
   uint32_t sp = 0;
+#ifdef RT_PROF  // profiling build: per-lane box steps / leaves, wave maxima, wave cycles (walk, leaves)
+  uint32_t pf_box = 0, pf_leaf = 0;
+  unsigned long long pf_leaf_cyc = 0;
+  const unsigned long long pf_t0 = __builtin_readcyclecounter();
+#endif
   for (;;) {
     // while-while: steps until the lane holds a leaf whose box was hit (or is done), then the
     // leaves with every lane that has one. (Postponing a lane's leaf and stepping on until every
@@ -1387,6 +1398,12 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
     while (ref < 0x8000u) {
       const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
       const uint32_t rr = refs[ref];
+#ifndef RT_CBVH_BRANCHY
+      // the stack top, read before the box tests so its latency overlaps them (slot 0 when the
+      // stack is empty: then unused)
+      const uint32_t top = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(
+          stack_b + (sp ? sp - sstep : 0u));
+#endif
       float tn0, tn1;
       const bool h0 = box(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
                           __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y), tn0);
@@ -1394,6 +1411,7 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
                           __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w), tn1);
       const bool first0 = h0 & (!h1 | (tn0 <= tn1));
       const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
+#ifdef RT_CBVH_BRANCHY
       if (h0 & h1) {
         stack[sp * sstride] = (uint16_t)(first0 ? r1 : r0);
         ++sp;
@@ -1406,20 +1424,72 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
       } else {
         ref = kDone;
       }
+#else
+      // Branch-free step: the farther hit child is written to the free slot above the top
+      // every step (kept only when both children are hit, i.e. pushed); visit the nearer hit
+      // child, else pop the top, else done. Same visiting order and stack contents as the
+      // branching form (RT_CBVH_BRANCHY).
+      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(stack_b + sp) =
+          (uint16_t)(first0 ? r1 : r0);
+      const bool any = h0 | h1;
+      ref = any ? (first0 ? r0 : r1) : (sp ? top : kDone);
+      sp = (h0 & h1) ? sp + sstep : ((any | (sp == 0u)) ? sp : sp - sstep);
+#endif
+#ifdef RT_PROF
+      ++pf_box;
+#endif
     }
     if (ref == kDone) break;
+#ifdef RT_PROF
+    ++pf_leaf;
+    const unsigned long long pf_l0 = __builtin_readcyclecounter();
+#endif
     const double closest_before = closest;
     obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin, cand);
     if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
+#ifdef RT_PROF
+    pf_leaf_cyc += __builtin_readcyclecounter() - pf_l0;
+#endif
+#ifdef RT_CBVH_BRANCHY
     if (sp > 0) {
       --sp;
       ref = stack[sp * sstride];
     } else {
       ref = kDone;
     }
+#else
+    if (sp > 0) {
+      sp -= sstep;
+      ref = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(stack_b + sp);
+    } else {
+      ref = kDone;
+    }
+#endif
   }
   flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
          (hit & (closest <= tmin * (1.0 + kTieRel)));
+#ifdef RT_PROF
+  {
+    const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
+    uint32_t mb = pf_box, ml = pf_leaf;
+    for (int k = 32; k > 0; k >>= 1) {
+      mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
+      ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
+    }
+    unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
+    const unsigned long long fl = __popcll(__ballot(flag));
+    atomicAdd(&pc[0], (unsigned long long)pf_box);
+    atomicAdd(&pc[2], (unsigned long long)pf_leaf);
+    if (prof_first_lane()) {
+      atomicAdd(&pc[1], (unsigned long long)mb);
+      atomicAdd(&pc[3], (unsigned long long)ml);
+      atomicAdd(&pc[4], 1ull);
+      atomicAdd(&pc[5], dt);
+      atomicAdd(&P.ops[52], fl);
+      atomicAdd(&P.ops[53 + (frame < 0 ? 0 : 1)], pf_leaf_cyc);  // lane 0's cycles in leaf tests
+    }
+  }
+#endif
   if (hit) {
     t_out = closest;
     if (MAIN) {

@@ -85,3 +85,22 @@ def scene_bytes(ops: dict, partial_bytes: int = 0) -> float:
 PEAK_FP64_VECTOR_TFLOPS = 78.6   # FP64 vector (half the 157.3 TF FP32 vector rate)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 PEAK_HBM_GBPS = 8000.0
+
+
+# The sources that determine rt_trace's machine code (ahead-of-time and scene-specialised). A PMC
+# traffic profile (profiles/pmc_traffic_<config>.json) records this hash; bench.py uses the
+# profile's bytes only while the hash matches the tree it runs from.
+KERNEL_SOURCES = ("rt_kernel.h", "rt_layout.h", "rt_rng.h", "rt_device.hip", "rt_jit.cpp",
+                  "rt_flatten.cpp", "rt_obvh.cpp")
+
+
+def kernel_source_sha16() -> str:
+    import hashlib
+    from pathlib import Path
+
+    csrc = Path(__file__).resolve().parent.parent / "csrc"
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        h.update(name.encode())
+        h.update((csrc / name).read_bytes())
+    return h.hexdigest()[:16]

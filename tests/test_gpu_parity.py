@@ -647,7 +647,7 @@ def test_multi_handle_renders_frames_without_reupload(gpu_available):
     With the box's one GPU listed 2 and 3 times the frame equals rt_render's bit for bit, also
     when accumulating; the second frame does no upload and no staging allocation
     (rt_multi_info counters)."""
-    import torch
+    from hip_buf import DevBuf
 
     blob, cam = rt.preset_blob("cornell_box", width=72, spp=16)
     ds = rt.DeviceScene(blob)
@@ -658,21 +658,22 @@ def test_multi_handle_renders_frames_without_reupload(gpu_available):
     ds.close()
     for devs in ([0, 0], [0, 0, 0]):
         m = rt.MultiScene(blob, devs)
-        out = torch.zeros(full.shape, dtype=torch.float32, device="cuda:0")
-        st1 = m.render_device(cam, rt.make_opts(cam, seed=4), out.data_ptr(), stats=True)
-        assert np.array_equal(out.cpu().numpy(), full), devs
+        out = DevBuf(full.shape)
+        st1 = m.render_device(cam, rt.make_opts(cam, seed=4), out.ptr, stats=True)
+        assert np.array_equal(out.download(), full), devs
         assert st1.samples == 72 * 72 * 16
         info1 = m.info()
-        out.zero_()
-        st2 = m.render_device(cam, rt.make_opts(cam, seed=4), out.data_ptr(), stats=True)
-        assert np.array_equal(out.cpu().numpy(), full), devs
+        out.upload(np.zeros_like(full))
+        st2 = m.render_device(cam, rt.make_opts(cam, seed=4), out.ptr, stats=True)
+        assert np.array_equal(out.download(), full), devs
         info2 = m.info()
         assert info1["uploads"] == info2["uploads"] == len(devs)
         assert info2["frames"] == 2 and info2["stage_allocs"] == info1["stage_allocs"] == 1
         print(f"rt_multi {devs}: frame 1 {st1.ms_total:.2f} ms, frame 2 {st2.ms_total:.2f} ms")
-        acc = torch.from_numpy(base.copy()).to("cuda:0")
-        m.render_device(cam, rt.make_opts(cam, seed=4, flags=0), acc.data_ptr(), stats=True)
-        assert np.array_equal(acc.cpu().numpy(), acc_one), devs
+        out.upload(base)
+        m.render_device(cam, rt.make_opts(cam, seed=4, flags=0), out.ptr, stats=True)
+        assert np.array_equal(out.download(), acc_one), devs
+        out.free()
         m.close()
 
 

@@ -7,14 +7,21 @@ FETCH_SIZE is reported raw (KiB -> bytes, no x2). Its stores are the f64 row par
 samples (24 B per lane-store) plus any scratch spill write-backs, so WRITE_SIZE is calibrated
 per launch against the known output bytes of one launch (argv[4], bench.py's
 algorithmic_bytes_per_launch): write_calibration = 1 means no extra write traffic.
-Usage: pmc_to_json.py OUT.json FETCH_GLOB WRITE_GLOB [ALGORITHMIC_WRITE_BYTES_PER_LAUNCH]"""
+Usage: pmc_to_json.py OUT.json FETCH_GLOB WRITE_GLOB [WORKSPACE_WRITE_BYTES_PER_LAUNCH [KERNEL_MS]]
+The JSON records the kernel-source hash of the profiled tree (surely_rt.roofline) and the
+profiled kernel time, so bench.py can refuse a stale profile."""
 import csv
 import glob
 import json
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "surely-raytracing_amd"))
+from surely_rt.roofline import kernel_source_sha16  # noqa: E402
 
 out = sys.argv[1]
 algo_write = float(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else None
+kernel_ms = float(sys.argv[5]) if len(sys.argv) > 5 and sys.argv[5] else None
 vals, n = {}, {}
 for name, pat in (("FETCH_SIZE", sys.argv[2]), ("WRITE_SIZE", sys.argv[3])):
     per = []
@@ -33,11 +40,13 @@ res = {
     "fetch_bytes": fb,
     "write_bytes": wb,
     "hbm_bytes_per_launch": fb + wb if fb is not None and wb is not None else None,
-    "algorithmic_write_bytes_per_launch": algo_write,
+    "workspace_write_bytes_per_launch": algo_write,
     "write_calibration": (wb / algo_write) if wb and algo_write else None,
+    "kernel_source_sha16": kernel_source_sha16(),
+    "profiled_kernel_ms": kernel_ms,
     "note": "FETCH_SIZE + WRITE_SIZE (KiB -> B) averaged over the rt_trace launches of the pass, "
             "raw (no x2: no 16-B streaming reads in this kernel); write_calibration = WRITE_SIZE "
-            "/ the launch's f64 output bytes (1 = no spill / extra write traffic)",
+            "/ the launch's f64 workspace stores (1 = no spill / extra write traffic)",
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))

@@ -41,3 +41,8 @@ for nm, b in (("top-level", 0), ("instance", 6)):
     print(f"    leaves:    {o[b + 2] / st.samples:.2f} lane/sample, wave-max {o[b + 3] / w:.1f} per walk, "
           f"SIMD eff {o[b + 2] / (64.0 * max(1, o[b + 3])):.3f}")
 print(f"  lanes re-walked in the reference order: {o[12]} ({o[12] / st.samples:.2e} per sample)")
+pc2 = (C.c_uint64 * 24)()
+for nm, k in (("top-level", 13), ("instance", 14)):
+    if o[k]:
+        print(f"  {nm} leaf tests (lane 0 of each wave, compact walk): {100 * o[k] / cyc.sum():.1f} % "
+              f"of path-loop wave-cycles")

@@ -10,8 +10,9 @@ mkdir -p $O
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o bench -- python3 bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline > $O/stats.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o bench -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-count --no-cpu-baseline > $O/fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o bench -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-count --no-cpu-baseline > $O/write.log 2>&1 || exit $?
-# algorithmic output bytes of one launch: bench.py's roofline.algorithmic_bytes_per_launch
-ALGO=$(python3 -c "import json,sys; l=[x for x in open('$O/stats.log') if x.startswith('{')]; print(json.loads(l[-1])['roofline']['algorithmic_bytes_per_launch'])")
-python3 tools_gpu/pmc_to_json.py $O/pmc_traffic_$CFG.json "$O/fetch/*counter_collection.csv" "$O/write/*counter_collection.csv" $ALGO > $O/traffic.log 2>&1 || exit $?
+# workspace bytes one launch stores and its kernel time: bench.py's roofline block
+ALGO=$(python3 -c "import json,sys; l=[x for x in open('$O/stats.log') if x.startswith('{')]; print(json.loads(l[-1])['roofline']['workspace_bytes_per_launch'])")
+KMS=$(python3 -c "import json,sys; l=[x for x in open('$O/stats.log') if x.startswith('{')]; r=json.loads(l[-1])['roofline']; print(r['kernel_ms'] / r['launches_per_render'])")
+python3 tools_gpu/pmc_to_json.py $O/pmc_traffic_$CFG.json "$O/fetch/*counter_collection.csv" "$O/write/*counter_collection.csv" $ALGO $KMS > $O/traffic.log 2>&1 || exit $?
 mkdir -p profiles && cp $O/pmc_traffic_$CFG.json profiles/
 timeout -k 10 600 python3 bench.py --config $CFG > $O/bench.log 2>&1
