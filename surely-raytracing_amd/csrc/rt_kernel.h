@@ -1168,8 +1168,13 @@ __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d
     const uint32_t cnt = batch ? (N[rec] >> 8) : 1u;
     gptr Q = batch ? N + rec + 4 : N + rec;
     uint32_t qrec = batch ? rec + 4 : rec;
+    // the next quad's axis-aligned form is loaded while this one is tested (past the batch's
+    // last quad the load reads the following record or the allocation's 256-byte tail, unused;
+    // C4 -1 %, profiles/r03_ab_c4_variants.log)
+    AQuad qn = load_aquad(Q);
     for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS, qrec += RTL_QUAD_WORDS) {
-      const AQuad q = load_aquad(Q);
+      const AQuad q = qn;
+      qn = load_aquad(Q + RTL_QUAD_WORDS);
       const uint32_t axis = RTL_QUAD_AXIS(q.h0);
       double t, a, b, dk;
       if (axis == 1u) {
@@ -1339,15 +1344,12 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   const lu4ptr nodes = reinterpret_cast<lu4ptr>(base);
   const lw_t refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
   const lw_t leaves = refs + n_int;
-#ifdef RT_CBVH_BRANCHY
+  // the lane's stack entries are blockDim.x u16 apart; sp is kept as a byte offset (a step adds
+  // or subtracts sstep instead of multiplying an entry count by the stride)
   typedef __attribute__((address_space(3))) uint16_t* ls_t;
-  const ls_t stack = reinterpret_cast<ls_t>((lbw_t)rt_lds + P.stack_lds_off) + threadIdx.x;
-  const uint32_t sstride = blockDim.x;
-#else
-  // the lane's stack entries are blockDim.x u16 apart; sp is kept as a byte offset
   const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 2u * threadIdx.x;
   const uint32_t sstep = 2u * blockDim.x;
-#endif
+  auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
@@ -1398,12 +1400,6 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
     while (ref < 0x8000u) {
       const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
       const uint32_t rr = refs[ref];
-#ifndef RT_CBVH_BRANCHY
-      // the stack top, read before the box tests so its latency overlaps them (slot 0 when the
-      // stack is empty: then unused)
-      const uint32_t top = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(
-          stack_b + (sp ? sp - sstep : 0u));
-#endif
       float tn0, tn1;
       const bool h0 = box(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
                           __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y), tn0);
@@ -1411,30 +1407,20 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
                           __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w), tn1);
       const bool first0 = h0 & (!h1 | (tn0 <= tn1));
       const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
-#ifdef RT_CBVH_BRANCHY
-      if (h0 & h1) {
-        stack[sp * sstride] = (uint16_t)(first0 ? r1 : r0);
-        ++sp;
+      // (A branch-free form -- the far child written to the free slot every step, the top read
+      // speculatively before the box tests -- was 3.5 % slower at C4: r03_ab_cbvh_branchfree_c4.)
+      if (h0 & h1) {  // both children hit: visit the nearer, push the other
+        *slot(sp) = (uint16_t)(first0 ? r1 : r0);
+        sp += sstep;
       }
       if (h0 | h1) {
         ref = first0 ? r0 : r1;
       } else if (sp > 0) {
-        --sp;
-        ref = stack[sp * sstride];
+        sp -= sstep;
+        ref = *slot(sp);
       } else {
         ref = kDone;
       }
-#else
-      // Branch-free step: the farther hit child is written to the free slot above the top
-      // every step (kept only when both children are hit, i.e. pushed); visit the nearer hit
-      // child, else pop the top, else done. Same visiting order and stack contents as the
-      // branching form (RT_CBVH_BRANCHY).
-      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(stack_b + sp) =
-          (uint16_t)(first0 ? r1 : r0);
-      const bool any = h0 | h1;
-      ref = any ? (first0 ? r0 : r1) : (sp ? top : kDone);
-      sp = (h0 & h1) ? sp + sstep : ((any | (sp == 0u)) ? sp : sp - sstep);
-#endif
 #ifdef RT_PROF
       ++pf_box;
 #endif
@@ -1450,21 +1436,12 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
 #ifdef RT_PROF
     pf_leaf_cyc += __builtin_readcyclecounter() - pf_l0;
 #endif
-#ifdef RT_CBVH_BRANCHY
-    if (sp > 0) {
-      --sp;
-      ref = stack[sp * sstride];
-    } else {
-      ref = kDone;
-    }
-#else
     if (sp > 0) {
       sp -= sstep;
-      ref = *reinterpret_cast<const __attribute__((address_space(3))) uint16_t*>(stack_b + sp);
+      ref = *slot(sp);
     } else {
       ref = kDone;
     }
-#endif
   }
   flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
          (hit & (closest <= tmin * (1.0 + kTieRel)));
@@ -1514,7 +1491,10 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
     int hf2 = -1;
     bool f2 = false;
     asm volatile("" : "+v"(z));
-    const bool h2 = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2);
+    const uint4 hd2 = ld4u((gptr)P.nodes + obvh);
+    const bool h2 = (P.cbvh_lds_off != ~0u && hd2.y != ~0u)
+                        ? cbvh_walk<MAIN>(P, hd2, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2)
+                        : obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2);
     asm volatile("" ::"v"(t2), "v"(hn2), "v"(h2), "v"(f2));
   }
 #endif
