@@ -95,8 +95,13 @@
  *   tree: n_int internal nodes of 48 bytes (both children's boxes as f32 [lo_x hi_x lo_y hi_y
  *   lo_z hi_z], outward-rounded as above), n_int u32 child-reference pairs (ref0 | ref1 << 16;
  *   ref < 0x8000: internal node, else leaf index ref & 0x7fff), n_int + 1 u32 leaf records.
- *   Internal-node depth <= RTL_CBVH_STACK (the walk's per-lane stack). */
-#define RTL_CBVH_STACK 24
+ *   Internal-node depth <= RTL_CBVH_STACK (the walk's per-lane stack).
+ * CBVH4 (A/B only, built with RT_CBVH4=1; header word 2 bit 31 set, bits 16-30 = n_int, bits
+ *   0-15 = root reference): the same tree collapsed to 4 children per node (compact_tree4): n_int nodes of 96 bytes
+ *   [lo_x 4][hi_x 4][lo_y 4][hi_y 4][lo_z 4][hi_z 4] (f32, child c in slot c; an empty slot is
+ *   the empty box +inf..-inf), n_int x 4 u16 child references (0xffff = empty), n_leaf u32 leaf
+ *   records. At most RTL_CBVH_STACK children pending on the walk's stack. */
+#define RTL_CBVH_STACK 32
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0
