@@ -87,9 +87,14 @@ variants-jocc: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=5 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w5.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_MIN_WAVES=6 -shared $(DEV_SRC) -o $(BUILD)/variants_jocc/librtmi355x_w6.so -lhiprtc
 
-# C4 walk ablations: the top-level / in-instance walk run twice
+# C4 ablations: every BVH leaf tested twice (variants-c4), the top-level / in-instance walk run
+# twice (variants-c4-walks)
 # (its cost); A/B with VARDIR=build/variants_c4 python tools_gpu/ab_variants.py 800 400 3 final_scene
 variants-c4: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_c4
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_LEAF2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_leaf2.so -lhiprtc
+
+variants-c4-walks: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_c4
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TWICE_BVH=1 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_twice1.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TWICE_BVH=2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_twice2.so -lhiprtc

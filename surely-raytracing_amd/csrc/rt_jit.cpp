@@ -615,6 +615,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_EXACT_PROBE
   opts.push_back("-DRT_EXACT_PROBE");
 #endif
+#ifdef RT_ABL_LEAF2
+  opts.push_back("-DRT_ABL_LEAF2");
+#endif
   // diagnostics: extra compiler options, space separated (register-allocation A/B)
   std::vector<std::string> extra;
   if (const char* e = std::getenv("RT_JIT_OPTS")) {

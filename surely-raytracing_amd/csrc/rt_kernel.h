@@ -1171,6 +1171,8 @@ __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d
     // the next quad's axis-aligned form is loaded while this one is tested (past the batch's
     // last quad the load reads the following record or the allocation's 256-byte tail, unused;
     // C4 -1 %, profiles/r03_ab_c4_variants.log)
+    // (Loading the record's first 80 bytes before its type is known, to start a sphere or a
+    // batch in one round trip, measured no faster: profiles/r03_ab_c4_leaf_variants.log.)
     AQuad qn = load_aquad(Q);
     for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS, qrec += RTL_QUAD_WORDS) {
       const AQuad q = qn;
@@ -1429,6 +1431,16 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
 #ifdef RT_PROF
     ++pf_leaf;
     const unsigned long long pf_l0 = __builtin_readcyclecounter();
+#endif
+#ifdef RT_ABL_LEAF2  // ablation build: every leaf tested twice (same result); the delta is their cost
+    {
+      double z = 0.0;
+      asm volatile("" : "+v"(z));
+      bool any = false;
+      auto nop = [&](bool v, double t, uint32_t) { any = any | (v & (t > z)); };
+      obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin + z, nop);
+      asm volatile("" ::"v"(any));
+    }
 #endif
     const double closest_before = closest;
     obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin, cand);
