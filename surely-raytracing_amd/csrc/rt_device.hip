@@ -188,6 +188,7 @@ struct rt_scene {
   unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
   unsigned int* queue = nullptr;
   int n_cu = 0;                 // compute units of the device
+  size_t mem_total = (size_t)8 << 30;  // device memory (hipMemGetInfo at creation)
   size_t lds_module_max = 64u << 10;  // LDS a module (hiprtc) launch may take (device limit)
   int resident_blocks[48] = {}; // per kernel variant: blocks resident per CU (0 = not queried)
   size_t resident_lds[48] = {};  // ... at this dynamic LDS size
@@ -304,6 +305,10 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
     e = hipDeviceGetAttribute(&lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
   if (e == hipSuccess && lds_block > 0)
     sc->lds_module_max = std::min<size_t>((size_t)lds_block, kLdsTotal);
+  if (e == hipSuccess) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) sc->mem_total = tot;
+  }
   if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
   if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
   for (int k = 0; k < rt_scene::kTraceRing && e == hipSuccess; ++k) {
@@ -666,9 +671,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   int64_t tail = max_blocks * (block / 64);
   if (const char* e = std::getenv("RT_TAIL_PAIRS")) tail = std::strtoll(e, nullptr, 10);
   tail = std::max<int64_t>(0, tail);
-  // Chunks of stratum rows keep the workspace under RT_WORKSPACE_MB (default 8 GiB): the
-  // 3840x2160 x 10000 spp frame takes several; 800x800 x 961 spp takes one (~0.7 GB).
-  size_t cap = (size_t)8192 << 20;
+  // Chunks of stratum rows keep the workspace under RT_WORKSPACE_MB (default 40 GiB, at most a
+  // quarter of the device's memory): an 8-GPU share of C5 (270 of 2160 rows x 3840, 10000 spp,
+  // ~33 GB) renders in one launch, the whole C5 frame on one GPU in several; 800x800 x 961 spp
+  // takes one (~2.1 GB).
+  size_t cap = std::min<size_t>((size_t)40960 << 20, sc->mem_total / 4);
   if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
   const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
   const size_t val_bytes = (size_t)64 * 3 * sizeof(double);  // one f64 RGB value per pixel
@@ -677,12 +684,18 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     const int64_t tb = std::min<int64_t>(pairs, tail);
     return ((size_t)(pairs - tb) * P.n_blk + (size_t)tb * S) * val_bytes;
   };
+  // a launch's f64 RGB outputs are indexed in 32 bits (end_sample) and its pools in 31
+  auto indexable = [&](int cn) {
+    const int64_t pairs = (int64_t)n_tiles * cn;
+    const int64_t tb = std::min<int64_t>(pairs, tail);
+    return ((pairs - tb) * P.n_blk + tb * (int64_t)S) * 64 < (1ll << 32) &&
+           pairs * P.n_blk <= 0x7fffffff;
+  };
   int chunk = n_sj;
-  while (chunk > 1 && tot_bytes + part_bytes(chunk) > cap) chunk = (chunk + 1) / 2;
+  while (chunk > 1 && (tot_bytes + part_bytes(chunk) > cap || !indexable(chunk)))
+    chunk = (chunk + 1) / 2;
   const size_t need = tot_bytes + part_bytes(chunk);
-  if ((int64_t)n_tiles * chunk * 64 * (int64_t)std::max(1, S) >= (1ll << 32) ||
-      (int64_t)n_tiles * chunk * P.n_blk > 0x7fffffff)
-    return set_err(RT_ERR_UNSUPPORTED, "grid too large");
+  if (!indexable(chunk)) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
   if (need > sc->work_bytes) {
     if (sc->work) HIP_TRY(hipFree(sc->work));
     sc->work = nullptr;

@@ -452,6 +452,26 @@ def test_baseline_config_frames_vs_oracle(gpu_available, cfg, name, kw, rows, op
         assert flips == 0
 
 
+@pytest.mark.timeout(300)
+def test_c5_eight_way_share_is_one_launch(gpu_available):
+    """BASELINE C5 (3840x2160, 10000 spp, depth 50) on 8 GPUs: one rank's cyclic share (rows
+    r, r + 8, ...: 270 rows, 10.4 G samples) renders in ONE path-kernel launch (the workspace
+    cap fits it) and gives the same rows as a two-chunk render of the same share."""
+    blob, cam = rt.preset_blob("cornell_box", width=3840, spp=10000, aspect=16.0 / 9.0)
+    ds = rt.DeviceScene(blob)
+    try:
+        acc, st = ds.render(cam, rt.make_opts(cam, seed=1, row_begin=3, row_step=8, n_rows=270))
+        assert st.launches == 1 and st.samples == 270 * 3840 * 10000
+        assert np.isfinite(acc).mean() > 0.9999 and acc.mean() > 0.0
+        print(f"C5 share: {st.ms_kernel:.0f} ms, {st.samples / st.ms_kernel / 1e3:.0f} Msamples/s")
+        rows = rt.make_opts(cam, seed=1, row_begin=3 + 8 * 100, row_step=8, n_rows=2)
+        two = _render_env(blob, cam, {"RT_WORKSPACE_MB": 64}, row_begin=rows.row_begin,
+                          row_step=8, n_rows=2)
+        assert np.array_equal(two, acc[100:102])
+    finally:
+        ds.close()
+
+
 def test_c5_camera_rows_vs_oracle(gpu_available):
     """C5 (book3 Cornell scene at 16:9, 3840x2160, 10000 spp, depth 50): the wide camera on two
     rows and a stratum subset (s_j 40..42 of 100: full-spp jitter, 300 samples per pixel)."""
