@@ -460,10 +460,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   P.inv_n_lights = sc->hdr.n_lights ? 1.0 / (double)sc->hdr.n_lights : 0.0;
   P.sphere_light0 = sc->sphere_light0;
   P.flags = opts->flags;
-#ifdef RT_PROF
-  const bool count = true;
-#else
   const bool count = (opts->flags & RT_FLAG_COUNT_OPS) != 0;
+#ifdef RT_PROF  // profiling build: the product kernels also fill the ops buffer (section cycles)
+  const bool ops_buf = true;
+#else
+  const bool ops_buf = count;
 #endif
   // VOL kernels: ConstantMedium nodes or an Isotropic material (also usable outside one)
   const bool vol = (sc->hdr.has_volume | sc->hdr.has_isotropic) != 0;
@@ -705,7 +706,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   }
   double* tot = (double*)sc->work;
   P.part = (double*)(sc->work + tot_bytes);
-  if (count) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
+  if (ops_buf) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
 #ifdef RT_PROF
   HIP_TRY(hipMemsetAsync(sc->ops + 40, 0, sizeof(unsigned long long) * 21, stream));
 #endif
@@ -754,7 +755,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     stats->samples = (uint64_t)n_px * (uint64_t)n_sj * (uint64_t)S;
     stats->out_bytes = out_bytes;
     stats->launches = launches;
-    if (count) {
+    if (ops_buf) {
       unsigned long long h[32];
       HIP_TRY(hipMemcpy(h, sc->ops, sizeof(h), hipMemcpyDeviceToHost));
       for (int k = 0; k < 32; ++k) stats->ops[k] = h[k];

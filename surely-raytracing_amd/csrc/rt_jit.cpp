@@ -490,7 +490,27 @@ std::string generate(const rtf::FlatScene& F, std::string* why) {
        "    (void)Nd; (void)hf; (void)p; (void)n;\n"
     << fo.str() << more << rest_out << "  }\n";
   if (!gen_lights_pdf(F, o, why)) return "";
-  o << "};\n";
+  // the scene's material kinds and light-list shape (rt_kernel.h kScene): shading code for what
+  // the scene lacks is compiled out. RT_NO_SCENE_SET=1 (diagnostics, A/B) keeps every case.
+  uint32_t sc = 0u;
+  for (size_t m = 0; m + RTL_MAT_WORDS <= F.mats.size(); m += RTL_MAT_WORDS) {
+    const uint32_t kind = F.mats[m] & 0xffu;
+    if (kind == RT_MAT_METAL) sc |= RTL_SC_METAL;
+    if (kind == RT_MAT_DIELECTRIC) sc |= RTL_SC_DIELECTRIC;
+    if (kind == RT_MAT_DIFFUSE_LIGHT) sc |= RTL_SC_LIGHT;
+  }
+  if (F.hdr.n_lights) sc |= RTL_SC_LIGHTS;
+  if (F.hdr.lights_nested) sc |= RTL_SC_LLIST;
+  for (uint32_t off : F.light_offs) {
+    const uint32_t ty = off < F.lights.size() ? (F.lights[off] & 0xffu) : 0u;
+    if (ty == RTL_SPHERE) sc |= RTL_SC_LSPHERE;
+    else if (ty != RTL_QUAD && ty != RTL_LLIST) sc |= RTL_SC_LOTHER;
+  }
+  const char* any = std::getenv("RT_NO_SCENE_SET");
+  if (any && *any && *any != '0') sc = RTL_SC_ANY;
+  char scb[64];
+  std::snprintf(scb, sizeof scb, "  static constexpr uint32_t kScene = 0x%xu;\n", sc);
+  o << scb << "};\n";
   return pre.str() + o.str();
 }
 

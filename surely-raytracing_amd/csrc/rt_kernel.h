@@ -1962,8 +1962,16 @@ __device__ __forceinline__ d3 xs_resolve(d3 L, uint32_t xs) {
 // the run-time interpreter of the flattened node sequence. Scene-specialised kernels (rt_jit.cpp)
 // supply a generated policy with the same signature and the same arithmetic.
 // VN > 0: the scene nests ConstantMedium records inside volume boundaries (that deep).
+// What a scene can contain, as far as the path loop's shading needs to know (a walker's kScene):
+// the interpreter walks any scene (every bit set, the run-time checks decide), a scene-specialised
+// walker (rt_jit.cpp) clears the bits of what its scene lacks, so the compiler drops that code and
+// the register copies its branches would cost. A cleared bit only removes a case that cannot occur.
+constexpr uint32_t kScMetal = RTL_SC_METAL, kScDielectric = RTL_SC_DIELECTRIC,
+                   kScLight = RTL_SC_LIGHT, kScLights = RTL_SC_LIGHTS, kScLList = RTL_SC_LLIST,
+                   kScLSphere = RTL_SC_LSPHERE, kScLOther = RTL_SC_LOTHER, kScAny = RTL_SC_ANY;
 template <int VN>
 struct TravInterpN {
+  static constexpr uint32_t kScene = kScAny;
   template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>
   static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,
                                                double& t, uint32_t& hn, int& hf, Rng& g,
@@ -2080,7 +2088,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   int q = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_jp = 0;
   bool tailp = false;  // the pool is a tail pool (one item per sample)
   bool more = true;    // the queue may still hold pools
-  const bool have_lights = P.n_lights > 0;
+  constexpr uint32_t SC = Trav::kScene;  // the scene's material kinds and light-list shape
+  const bool have_lights = (SC & kScLights) && P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
   constexpr int NB = BlockOf<BVH>::value;
   // per-lane f64 running sum of the item in flight (segment items: the block's samples so far)
@@ -2339,13 +2348,13 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     Trav::frame_out(T.nodes, hf, p, normal);  // back to world space
     const uint32_t kind = mh.x & 0xffu;
     PROF(3);
-    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
+    if ((SC & kScLight) && kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
       term = true;
       break;
     }
-    if (kind == RT_MAT_METAL) {  // material.rs:124-134
+    if ((SC & kScMetal) && kind == RT_MAT_METAL) {  // material.rs:124-134
       C.inc(RT_OP_METAL);
       d3 reflected = reflect(unit_vector(rd), normal);
       d3 ruv = random_unit_vector(g);
@@ -2360,7 +2369,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // running two exclusive branches. Per lane the arithmetic and the draw order are exactly
     // those of the separate branches.
     PROF(4);
-    const bool diel = kind == RT_MAT_DIELECTRIC;
+    const bool diel = (SC & kScDielectric) && kind == RT_MAT_DIELECTRIC;
     const bool iso = VOL && kind == RT_MAT_ISOTROPIC;  // VOL kernels: volumes or Isotropic
     C.inc(diel ? RT_OP_DIELECTRIC : (iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN));
     // unit(r_in.direction) (material.rs:170) or CosinePDF's w = unit(normal) (pdf.rs:58-62)
@@ -2370,7 +2379,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // first sqrt: the dielectric's sin(theta) (material.rs:173) or cos_theta_max of the first
     // sphere light at p (object.rs:196, 205-207), shared by Sphere::random and pdf_value
     double sq_in = fma(-cos_t, cos_t, 1.0);
-    if (P.sphere_light0 >= 0) {
+    if ((SC & kScLSphere) && P.sphere_light0 >= 0) {
       const TP S0 = T.lights + T.loffs[P.sphere_light0];
       const d3 cmo = ld3(S0, 0) - p;
       const double r0 = ldd(S0, 3);
@@ -2402,7 +2411,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         li = P.lights_is_list ? rnd_index(g, P.n_lights) : 0u;
         L = T.lights + T.loffs[li];
         ltype = L[0] & 0xffu;
-        while (ltype == RTL_LLIST) {  // a nested HittableList: random_int pick (hittable.rs:126-129)
+        while ((SC & kScLList) && ltype == RTL_LLIST) {  // a nested HittableList: random_int pick (hittable.rs:126-129)
           li = L[1] + rnd_index(g, L[0] >> 8);
           L = T.lights + T.loffs[li];
           ltype = L[0] & 0xffu;
@@ -2413,7 +2422,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const d3 un = uu;
       if (iso && !light_branch) {
         dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
-      } else if (light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
+      } else if ((SC & kScLOther) && light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
         dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
       } else {
         // Quad::random (object.rs:503-506), Sphere::random / random_to_sphere (204-212, 122-132)
@@ -2421,7 +2430,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         // one ONB, one sincos, selects instead of divergent branches.
         const double r1 = rnd(g), r2 = rnd(g);
         const bool lq = light_branch && ltype == RTL_QUAD;
-        const bool ls = light_branch && ltype == RTL_SPHERE;
+        const bool ls = (SC & kScLSphere) && light_branch && ltype == RTL_SPHERE;
         d3 c = ls ? ld3(L, 0) : p;
         d3 wdir = c - p;  // Sphere::random direction (object.rs:205)
         d3 w = ls ? unit_vector(wdir) : un;

@@ -133,6 +133,16 @@
  *   METAL: c = albedo, param = fuzz; DIELECTRIC: c = tint, param = ir, d4 = 1/ir,
  *   d5 / d6 = Schlick r0 for the front / back face ratio (material.rs:150-158, 166-191; the same
  *   IEEE divisions the reference performs per hit, done once on the host) */
+/* Scene set (a walker's kScene, rt_kernel.h trace_body): material kinds and light-list shapes a
+ * scene contains; a scene-specialised walker (rt_jit.cpp) clears the bits of what it lacks. */
+#define RTL_SC_METAL 0x1u
+#define RTL_SC_DIELECTRIC 0x2u
+#define RTL_SC_LIGHT 0x4u       /* a DiffuseLight material                          */
+#define RTL_SC_LIGHTS 0x8u      /* a non-empty light list                           */
+#define RTL_SC_LLIST 0x10u      /* a HittableList nested in the light list         */
+#define RTL_SC_LSPHERE 0x20u    /* a sphere in the light list                       */
+#define RTL_SC_LOTHER 0x40u     /* a light that is neither quad, sphere nor list    */
+#define RTL_SC_ANY 0xffffffffu
 #define RTL_MAT_WORDS 20
 #define RTL_MATF_NEEDS_UV 0x100u
 /* texture (12 words): [kind][a][b][c] d0-3
