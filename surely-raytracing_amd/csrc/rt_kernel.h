@@ -2398,7 +2398,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr)
     const bool refl = tir || r0s + (1.0 - r0s) * pow5_cr(1.0 - cos_t) > u0;
     const bool light_branch = !diel && have_lights && u0 < 0.5;
-    d3 dir = mk(0., 0., 0.), factor = mk(0., 0., 0.);
+    d3 dir, factor;  // set on both arms below
     double cos_sl = cos_sl0;
     if (!diel) {
       d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
@@ -2498,8 +2498,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         factor = beta;
       }
 #endif
-    }
-    if (diel) {
+    } else {
       // reflect (vec3.rs:219-221) or refract (vec3.rs:223-229; its cos_theta is cos_t)
       const d3 perp = ratio * vfma(cos_t, normal, uu);
       const d3 refr = vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), normal, perp);
