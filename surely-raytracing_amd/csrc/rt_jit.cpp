@@ -537,7 +537,7 @@ std::string kernel_source(const std::string& walker, const Flags& f) {
       << "}  // namespace rtk\nusing namespace rtk;\n"
          "extern \"C\" __global__ __launch_bounds__(BlockOf<" << b(f.bvh) << ">::value, "
          "(MinWaves<" << b(f.vol) << ", " << b(f.tex) << ", " << b(f.bvh)
-      << ">::value)) void rt_trace_jit(TraceParams P) {\n"
+      << ", true>::value)) void rt_trace_jit(TraceParams P) {\n"
       << "  trace_body<false, " << b(f.vol) << ", " << b(f.tex) << ", " << b(f.bvh) << ", "
       << b(f.staged) << ", " << b(f.volb) << ", " << b(f.voli) << ", TravGen>(P);\n}\n";
   return src.str();
@@ -598,6 +598,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #endif
 #ifdef RT_MIN_WAVES_BVH
   opts.push_back("-DRT_MIN_WAVES_BVH=" RTJ_STR(RT_MIN_WAVES_BVH));
+#endif
+#ifdef RT_MIN_WAVES_GEN
+  opts.push_back("-DRT_MIN_WAVES_GEN=" RTJ_STR(RT_MIN_WAVES_GEN));
 #endif
 #ifdef RT_BLOCK_BVH
   opts.push_back("-DRT_BLOCK_BVH=" RTJ_STR(RT_BLOCK_BVH));

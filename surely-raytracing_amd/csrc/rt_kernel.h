@@ -70,9 +70,15 @@ constexpr size_t kLdsTotal = 160u << 10;
 #ifndef RT_MIN_WAVES_BVH
 #define RT_MIN_WAVES_BVH 3
 #endif
-template <bool VOL, bool TEX, bool BVH>
+// Scene-specialised kernels without a BVH (rt_jit.cpp) carry less code (the scene set, §4.1b
+// of DESIGN.md: cornell_box 90, cornell_smoke 100 VGPRs) and run five waves per SIMD:
+// cornell_smoke 96.65 -> 95.78 ms, cornell_box unchanged (profiles/r03_ab_occ_*.log).
+#ifndef RT_MIN_WAVES_GEN
+#define RT_MIN_WAVES_GEN 5
+#endif
+template <bool VOL, bool TEX, bool BVH, bool GEN = false>
 struct MinWaves {
-  static constexpr int value = BVH ? RT_MIN_WAVES_BVH : RT_MIN_WAVES;
+  static constexpr int value = BVH ? RT_MIN_WAVES_BVH : (GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES);
 };
 
 struct d3 {
