@@ -93,6 +93,9 @@ variants-jocc: $(DEV_SRC) $(DEV_HDR)
 variants-c4: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_c4
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_LEAF2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_leaf2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOISE2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_noise2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_FRESH2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_fresh2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_HIT2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_hit2.so -lhiprtc
 
 variants-c4-walks: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_c4

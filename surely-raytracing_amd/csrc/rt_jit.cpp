@@ -641,6 +641,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_LEAF2
   opts.push_back("-DRT_ABL_LEAF2");
 #endif
+#ifdef RT_ABL_NOISE2
+  opts.push_back("-DRT_ABL_NOISE2");
+#endif
   // diagnostics: extra compiler options, space separated (register-allocation A/B)
   std::vector<std::string> extra;
   if (const char* e = std::getenv("RT_JIT_OPTS")) {

@@ -1301,18 +1301,20 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
 #ifdef RT_PROF
   {
     const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
-    uint32_t mb = pf_box, ml = pf_leaf;
+    uint32_t mb = pf_box, ml = pf_leaf, sb = pf_box, sl = pf_leaf;  // wave max and sum
     for (int k = 32; k > 0; k >>= 1) {
       mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
       ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
+      sb += (uint32_t)__shfl_xor((int)sb, k);
+      sl += (uint32_t)__shfl_xor((int)sl, k);
     }
     // P.ops[40 + ...] (past the pool-queue word; rt_scene_prof_counters): per walk kind
     // (0: world frame, 1: instance frame) 6 counters
     unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
     const unsigned long long fl = __popcll(__ballot(flag));
-    atomicAdd(&pc[0], (unsigned long long)pf_box);
-    atomicAdd(&pc[2], (unsigned long long)pf_leaf);
     if (prof_first_lane()) {
+      atomicAdd(&pc[0], (unsigned long long)sb);
+      atomicAdd(&pc[2], (unsigned long long)sl);
       atomicAdd(&pc[1], (unsigned long long)mb);
       atomicAdd(&pc[3], (unsigned long long)ml);
       atomicAdd(&pc[4], 1ull);
@@ -1466,16 +1468,18 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
 #ifdef RT_PROF
   {
     const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
-    uint32_t mb = pf_box, ml = pf_leaf;
+    uint32_t mb = pf_box, ml = pf_leaf, sb = pf_box, sl = pf_leaf;  // wave max and sum
     for (int k = 32; k > 0; k >>= 1) {
       mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
       ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
+      sb += (uint32_t)__shfl_xor((int)sb, k);
+      sl += (uint32_t)__shfl_xor((int)sl, k);
     }
     unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
     const unsigned long long fl = __popcll(__ballot(flag));
-    atomicAdd(&pc[0], (unsigned long long)pf_box);
-    atomicAdd(&pc[2], (unsigned long long)pf_leaf);
     if (prof_first_lane()) {
+      atomicAdd(&pc[0], (unsigned long long)sb);
+      atomicAdd(&pc[2], (unsigned long long)sl);
       atomicAdd(&pc[1], (unsigned long long)mb);
       atomicAdd(&pc[3], (unsigned long long)ml);
       atomicAdd(&pc[4], 1ull);
@@ -1784,6 +1788,14 @@ __device__ d3 tex_value(const TraceParams& P, const TT& T, uint32_t id, double u
       double turb = h.y < P.n_perlin_lds
                         ? perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
                         : perlin_turb_global(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
+#ifdef RT_ABL_NOISE2  // ablation build: the turbulence evaluated twice (same result; its cost)
+      {
+        d3 s2 = s;
+        asm volatile("" : "+v"(s2.x));
+        const double t2 = perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s2);
+        asm volatile("" ::"v"(t2));
+      }
+#endif
       double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
       return mk(k, k, k);
     }

@@ -109,3 +109,39 @@ def test_volume_boundary_queries_generated():
     assert state == 1, src
     structs = re.findall(r"struct (VolTwo_\d+) \{", src)
     assert len(structs) == 2 and all("sqrt_nr(disc)" in src for _ in structs)
+
+
+def _scene_set(src):
+    m = re.search(r"static constexpr uint32_t kScene = 0x([0-9a-f]+)u;", src)
+    assert m, "walker without a scene set"
+    return int(m.group(1), 16)
+
+
+# rt_layout.h RTL_SC_*
+SC_METAL, SC_DIEL, SC_LIGHT, SC_LIGHTS, SC_LLIST, SC_LSPHERE, SC_LOTHER = (1, 2, 4, 8, 16, 32, 64)
+
+
+@pytest.mark.parametrize("name,expect", [
+    # book3 Cornell box (main.rs:417-494): lambertian walls and box, a light, a glass sphere that
+    # is also the second light-list entry
+    ("cornell_box", SC_DIEL | SC_LIGHT | SC_LIGHTS | SC_LSPHERE),
+    # book2 smoke boxes (main.rs:514-598): no light list (render_par), isotropic media
+    ("cornell_smoke", SC_LIGHT),
+    # book2 final scene (main.rs:603-712): every material kind, no light list
+    ("final_scene", SC_METAL | SC_DIEL | SC_LIGHT),
+])
+def test_scene_set_of_presets(name, expect):
+    """The generated walker's kScene names exactly the material kinds and light-list shapes the
+    scene holds (rt_jit.cpp): the path kernel compiles out the shading of everything else, so a
+    bit may only be cleared for a case the scene cannot reach."""
+    blob, cam = rt.preset_blob(name, width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1, src
+    assert _scene_set(src) == expect
+
+
+def test_scene_set_diagnostic_keeps_every_case(monkeypatch):
+    monkeypatch.setenv("RT_NO_SCENE_SET", "1")
+    blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
+    state, src = rt.jit_check(blob)
+    assert state == 1 and _scene_set(src) == 0xFFFFFFFF
