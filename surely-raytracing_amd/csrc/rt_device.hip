@@ -46,20 +46,22 @@ __global__ __launch_bounds__(BlockOf<BVH>::value, (MinWaves<VOL, TEX, BVH>::valu
   trace_body<COUNT, VOL, TEX, BVH, STAGED, VOLB, VOLI, TravInterpN<VN>>(P);
 }
 
-// Per pixel, in the reference's sample order (s_j, then s_i: render.rs:185-189): the f64 partial
-// of each block of kPoolSi samples (a segment item's running sum, or the sequential sum of a tail
-// block's per-sample values: the same running sum, bit for bit) added into one running total.
-// The reference adds every sample into that total; here a block's samples are summed first, so
-// the association differs from the reference's only between blocks. One wave per 8x8 tile,
-// lane = pixel of the tile: each load instruction reads 64 * 8 contiguous bytes. Chunked calls
-// carry the running total in `tot`. mode: bit0 first chunk, bit1 last chunk (write accum), bit2
-// overwrite.
-constexpr int kRedU = 8;  // partials loaded ahead per step of rt_reduce
+// Per pixel, in the reference's sample order (s_j, then s_i: render.rs:185-189): for each
+// stratum row s_j its total R = ((p_0 + p_1) + p_2) + ... over the block partials p_b (a row
+// item's R as the lane formed it; a segment pair's from its block partials; a tail pair's from
+// the sequential sums of its blocks' samples: the same running sums, bit for bit), added into
+// one running total. The reference adds every sample into that total; here a block's samples are
+// summed first and a row's blocks next, so the association differs from the reference's only
+// between blocks and between rows, and it does not depend on how the launch split its pairs into
+// row, segment and tail items. One wave per 8x8 tile, lane = pixel of the tile: each load
+// instruction reads 64 * 8 contiguous bytes. Chunked calls carry the running total in `tot`.
+// mode: bit0 first chunk, bit1 last chunk (write accum), bit2 overwrite.
+constexpr int kRedU = 8;  // values loaded ahead per step of rt_reduce
 __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part,
                                                  double* __restrict__ tot,
                                                  float* __restrict__ accum, int W, int n_rows,
                                                  int tiles_x, int n_tiles, int n_sj, int S,
-                                                 int n_pairs_a, int mode) {
+                                                 int n_pairs_r, int n_pairs_a, int mode) {
   const int tile_id = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int pv = threadIdx.x & 63;
   if (tile_id >= n_tiles) return;
@@ -76,32 +78,57 @@ __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part
     t1 = tot[3 * i + 1];
     t2 = tot[3 * i + 2];
   }
-  // segment pairs of this tile: their partials are consecutive (stride 64 values), s_j-major
-  const int k_a = max(0, min(n_sj, n_pairs_a - tile_id * n_sj));
-  const double* r = part + ((size_t)tile_id * n_sj * n_blk * 64 + pv) * 3;
-  const int M = k_a * n_blk;
-  int m = 0;
-  // loads first, then the in-order adds: 24 loads in flight per lane (a share's few waves are
-  // otherwise bound by one load's latency per partial)
-  for (; m + kRedU <= M; m += kRedU) {
-    double v[kRedU][3];
+  const int q0 = tile_id * n_sj;  // this tile's pairs q0 .. q0 + n_sj - 1 (s_j order)
+  const int k_r = max(0, min(n_sj, n_pairs_r - q0)), k_a = max(0, min(n_sj, n_pairs_a - q0));
+  int k = 0;
+  // row pairs: one total each, 64 values apart; loads first, then the in-order adds (a share's
+  // few waves are otherwise bound by one load's latency per value)
+  {
+    const double* r = part + ((size_t)q0 * 64 + pv) * 3;
+    for (; k + kRedU <= k_r; k += kRedU) {
+      double v[kRedU][3];
 #pragma unroll
-    for (int u = 0; u < kRedU; ++u) {
-      const double* e = r + (size_t)(m + u) * 192;
-      v[u][0] = e[0], v[u][1] = e[1], v[u][2] = e[2];
+      for (int u = 0; u < kRedU; ++u) {
+        const double* e = r + (size_t)(k + u) * 192;
+        v[u][0] = e[0], v[u][1] = e[1], v[u][2] = e[2];
+      }
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) t0 += v[u][0], t1 += v[u][1], t2 += v[u][2];
     }
+    for (; k < k_r; ++k) {
+      const double* e = r + (size_t)k * 192;
+      t0 += e[0], t1 += e[1], t2 += e[2];
+    }
+  }
+  // segment pairs: the row total of n_blk block partials
+  for (; k < k_a; ++k) {
+    const int q = q0 + k;
+    const double* r =
+        part + (((size_t)n_pairs_r + (size_t)(q - n_pairs_r) * n_blk) * 64 + pv) * 3;
+    double r0 = r[0], r1 = r[1], r2 = r[2];
+    int b = 1;
+    for (; b + kRedU <= n_blk; b += kRedU) {
+      double v[kRedU][3];
 #pragma unroll
-    for (int u = 0; u < kRedU; ++u) t0 += v[u][0], t1 += v[u][1], t2 += v[u][2];
+      for (int u = 0; u < kRedU; ++u) {
+        const double* e = r + (size_t)(b + u) * 192;
+        v[u][0] = e[0], v[u][1] = e[1], v[u][2] = e[2];
+      }
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) r0 += v[u][0], r1 += v[u][1], r2 += v[u][2];
+    }
+    for (; b < n_blk; ++b) {
+      const double* e = r + (size_t)b * 192;
+      r0 += e[0], r1 += e[1], r2 += e[2];
+    }
+    t0 += r0, t1 += r1, t2 += r2;
   }
-  for (; m < M; ++m) {
-    const double* e = r + (size_t)m * 192;
-    t0 += e[0], t1 += e[1], t2 += e[2];
-  }
-  // tail pairs: per-sample values, summed per block of kPoolSi samples
-  for (int k = k_a; k < n_sj; ++k) {
-    const size_t q = (size_t)tile_id * n_sj + k;
-    const double* rt =
-        part + ((size_t)n_pairs_a * n_blk * 64 + (q - n_pairs_a) * (size_t)S * 64 + pv) * 3;
+  // tail pairs: per-sample values, summed per block of kPoolSi samples, then the blocks
+  const size_t tail0 = (size_t)n_pairs_r + (size_t)(n_pairs_a - n_pairs_r) * n_blk;
+  for (; k < n_sj; ++k) {
+    const int q = q0 + k;
+    const double* rt = part + ((tail0 + (size_t)(q - n_pairs_a) * S) * 64 + pv) * 3;
+    double R0 = 0.0, R1 = 0.0, R2 = 0.0;
     for (int s0 = 0; s0 < S; s0 += kPoolSi) {
       const int n = min(kPoolSi, S - s0);
       double v[kPoolSi][3];
@@ -116,8 +143,13 @@ __global__ __launch_bounds__(256) void rt_reduce(const double* __restrict__ part
 #pragma unroll
       for (int u = 0; u < kPoolSi; ++u)
         if (u < n) r0 += v[u][0], r1 += v[u][1], r2 += v[u][2];
-      t0 += r0, t1 += r1, t2 += r2;
+      if (s0 == 0) {
+        R0 = r0, R1 = r1, R2 = r2;
+      } else {
+        R0 += r0, R1 += r1, R2 += r2;
+      }
     }
+    t0 += R0, t1 += R1, t2 += R2;
   }
   float* a = accum + 3 * i;
   if (mode & 2) {
@@ -471,9 +503,10 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   const bool tex = sc->hdr.has_textures != 0;
   const bool bvh = sc->hdr.has_bvh != 0;
   const int block = bvh ? kBlockBvh : kBlock;
-  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc), the op
-  // counters, slack for the profiling build; the dynamic LDS holds the staged tables
-  const size_t static_lds = (size_t)block * 24 + 512 + (count ? 128 : 0);
+  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc, and the row
+  // totals sh_row of non-BVH kernels), the op counters, slack for the profiling build; the
+  // dynamic LDS holds the staged tables
+  const size_t static_lds = (size_t)block * (bvh ? 24 : 48) + 512 + (count ? 128 : 0);
   // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
   // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.
   const uint32_t used_perlins = sc->hdr.has_textures ? sc->hdr.n_perlins : 0u;
@@ -663,35 +696,55 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     sc->resident_lds[kslot] = lds_bytes;
   }
   const int64_t max_blocks = (int64_t)sc->resident_blocks[kslot] * std::max(1, sc->n_cu);
-  // Outputs (TraceParams::part): one f64 RGB partial per (pixel, s_j, block) of the segment
-  // pairs and one per sample of the tail pairs. The tail is about one pair per resident wave (a
-  // pair is 64 x sqrt_spp paths): when the segment pools run out, lanes still finishing a
-  // segment have ~kPoolSi / 2 samples left, and the tail's single samples keep the other lanes
-  // busy meanwhile.
-  // RT_TAIL_PAIRS overrides it (tests: the image does not depend on the split).
-  int64_t tail = max_blocks * (block / 64);
-  if (const char* e = std::getenv("RT_TAIL_PAIRS")) tail = std::strtoll(e, nullptr, 10);
-  tail = std::max<int64_t>(0, tail);
-  // Chunks of stratum rows keep the workspace under RT_WORKSPACE_MB (default 40 GiB, at most a
-  // quarter of the device's memory): an 8-GPU share of C5 (270 of 2160 rows x 3840, 10000 spp,
-  // ~33 GB) renders in one launch, the whole C5 frame on one GPU in several; 800x800 x 961 spp
-  // takes one (~2.1 GB).
-  size_t cap = std::min<size_t>((size_t)40960 << 20, sc->mem_total / 4);
-  if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
+  // Outputs (TraceParams::part): one f64 RGB value per (pixel, s_j) of the row pairs, one per
+  // (pixel, s_j, block) of the segment pairs and one per sample of the tail pairs.
+  //  * A launch of many pairs per resident wave (a whole frame on one GPU: C2 has 60) renders
+  //    row items, then a band of segment items about four pairs per resident wave long, then a
+  //    tail of single samples an eighth of a pair per wave long. When the row pools run out, the
+  //    lanes still finishing a row have up to sqrt_spp paths left (rows through glass take
+  //    several times the mean), and the band keeps the other lanes busy meanwhile; the tail
+  //    does the same for the segments' last ~kPoolSi / 2 samples. The workspace is then about
+  //    one value per (pixel, s_j): C2 0.59 GB instead of 2.1.
+  //  * Smaller launches (an N-way share, chunks) balance better without rows (C2 over 8 GPUs:
+  //    0.940 of ideal with segments, 0.894 with half the pairs as rows, profiles/
+  //    r03_scaling_probe_*.log): segment items, then a tail of one pair per resident wave.
+  //  * BVH kernels keep their LDS for the compact trees and render no rows. Row items need
+  //    s_j < 2^15 (lane key).
+  // RT_SEG_PAIRS (rows with that band) and RT_TAIL_PAIRS override the sizes (tests: the image
+  // does not depend on the split).
+  const int64_t res_waves = max_blocks * (block / 64);
+  const bool rows_ok = !bvh && S < 32768;
+  const char* seg_env = std::getenv("RT_SEG_PAIRS");
+  const char* tail_env = std::getenv("RT_TAIL_PAIRS");
+  struct Split {
+    int64_t pairs, r, a, values;  // row pairs [0, r), segment pairs [r, a), tail [a, pairs)
+  };
+  auto split = [&](int cn) {
+    Split sp;
+    sp.pairs = (int64_t)n_tiles * cn;
+    const bool rows = rows_ok && (seg_env ? true : sp.pairs >= 24 * res_waves);
+    int64_t tail = rows ? std::max<int64_t>(1, res_waves / 8) : res_waves;
+    if (tail_env) tail = std::strtoll(tail_env, nullptr, 10);
+    const int64_t band = seg_env ? std::strtoll(seg_env, nullptr, 10) : 4 * res_waves;
+    const int64_t tb = std::min<int64_t>(sp.pairs, std::max<int64_t>(0, tail));
+    sp.a = sp.pairs - tb;
+    sp.r = rows ? std::max<int64_t>(0, sp.a - std::max<int64_t>(0, band)) : 0;
+    sp.values = sp.r + (sp.a - sp.r) * P.n_blk + tb * S;  // 64-value slots
+    return sp;
+  };
   const size_t tot_bytes = (n_px * 3 * sizeof(double) + 255) & ~(size_t)255;
   const size_t val_bytes = (size_t)64 * 3 * sizeof(double);  // one f64 RGB value per pixel
-  auto part_bytes = [&](int cn) {
-    const int64_t pairs = (int64_t)n_tiles * cn;
-    const int64_t tb = std::min<int64_t>(pairs, tail);
-    return ((size_t)(pairs - tb) * P.n_blk + (size_t)tb * S) * val_bytes;
-  };
+  auto part_bytes = [&](int cn) { return (size_t)split(cn).values * val_bytes; };
   // a launch's f64 RGB outputs are indexed in 32 bits (end_sample) and its pools in 31
   auto indexable = [&](int cn) {
-    const int64_t pairs = (int64_t)n_tiles * cn;
-    const int64_t tb = std::min<int64_t>(pairs, tail);
-    return ((pairs - tb) * P.n_blk + tb * (int64_t)S) * 64 < (1ll << 32) &&
-           pairs * P.n_blk <= 0x7fffffff;
+    const Split sp = split(cn);
+    return sp.values * 64 < (1ll << 32) && sp.r + (sp.pairs - sp.r) * P.n_blk <= 0x7fffffff;
   };
+  // Chunks of stratum rows keep the workspace under RT_WORKSPACE_MB (default 40 GiB, at most a
+  // quarter of the device's memory): the whole C5 frame (3840 x 2160, 10000 spp, ~19 GB of row
+  // totals) renders in one launch; 800x800 x 961 spp takes one (~0.59 GB).
+  size_t cap = std::min<size_t>((size_t)40960 << 20, sc->mem_total / 4);
+  if (const char* e = std::getenv("RT_WORKSPACE_MB")) cap = (size_t)std::strtoull(e, nullptr, 10) << 20;
   int chunk = n_sj;
   while (chunk > 1 && (tot_bytes + part_bytes(chunk) > cap || !indexable(chunk)))
     chunk = (chunk + 1) / 2;
@@ -717,12 +770,12 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     const int cn = std::min(chunk, sj0 + n_sj - c0);
     out_bytes += part_bytes(cn);
     ++launches;
-    const int64_t pairs = (int64_t)n_tiles * cn;
-    const int64_t tb = std::min<int64_t>(pairs, tail);
+    const Split sp = split(cn);
     P.sj0 = c0;
     P.n_sj = cn;
-    P.n_pairs_a = (int)(pairs - tb);
-    P.n_pools = (int)(pairs * P.n_blk);
+    P.n_pairs_r = (int)sp.r;
+    P.n_pairs_a = (int)sp.a;
+    P.n_pools = (int)(sp.r + (sp.pairs - sp.r) * P.n_blk);
     // persistent grid: as many waves as the device holds at once (never more than pools)
     const int64_t blocks = std::min(max_blocks, ((int64_t)P.n_pools + (block / 64) - 1) / (block / 64));
     HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
@@ -742,7 +795,8 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     const int mode = (c0 == sj0 ? 1 : 0) | (c0 + cn == sj0 + n_sj ? 2 : 0) |
                      ((opts->flags & RT_FLAG_OVERWRITE) ? 4 : 0);
     hipLaunchKernelGGL(rt_reduce, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, stream, P.part,
-                       tot, accum, W, opts->n_rows, P.tiles_x, n_tiles, cn, S, P.n_pairs_a, mode);
+                       tot, accum, W, opts->n_rows, P.tiles_x, n_tiles, cn, S, P.n_pairs_r,
+                       P.n_pairs_a, mode);
     HIP_TRY(hipGetLastError());
   }
   ++sc->n_render;

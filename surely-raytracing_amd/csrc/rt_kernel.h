@@ -310,15 +310,18 @@ struct TraceParams {
   const uint32_t* __restrict__ lights;
   const uint32_t* __restrict__ light_offs;
   const uint8_t* __restrict__ texels;
-  // f64 RGB outputs of the launch (rt_reduce sums them): first the segment partials of the
-  // segment pairs [0, n_pairs_a) (index (pair * n_blk + blk) * 64 + pv), then the per-sample
-  // values of the tail pairs (index (n_pairs_a * n_blk + (pair - n_pairs_a) * sqrt_spp + s_i) *
-  // 64 + pv)
+  // f64 RGB outputs of the launch (rt_reduce sums them), 64 values (one per pixel of the tile)
+  // per slot: the row totals of the row pairs [0, n_pairs_r) (slot = pair), the block partials
+  // of the segment pairs [n_pairs_r, n_pairs_a) (slot = n_pairs_r + (pair - n_pairs_r) * n_blk +
+  // blk), then the per-sample values of the tail pairs (slot = n_pairs_r + (n_pairs_a -
+  // n_pairs_r) * n_blk + (pair - n_pairs_a) * sqrt_spp + s_i). A row or segment pool's id is
+  // its slot.
   double* __restrict__ part;
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  int n_pools;    // pools of this launch: pairs * n_blk, pool id = pair * n_blk + blk
-  int n_pairs_a;  // (tile, s_j) pairs rendered as segment items (the rest: one item per sample)
+  int n_pools;    // pools of this launch: n_pairs_r + (pairs - n_pairs_r) * n_blk
+  int n_pairs_r;  // (tile, s_j) pairs rendered as row items (one item per pixel, all s_i)
+  int n_pairs_a;  // pairs [n_pairs_r, n_pairs_a): segment items; the rest one item per sample
   int n_blk;      // s_i blocks (segments) per pair: ceil(sqrt_spp / kPoolSi)
   uint32_t root, n_lights, lights_is_list, flags;
   uint32_t lights_nested;  // some light entry is a nested HittableList (RTL_LLIST)
@@ -2092,26 +2095,37 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   } while (0)
 #endif
   // Persistent waves over a global pool queue. A pool is one 8x8 pixel tile x
-  // one stratum row s_j x one block of kPoolSi stratum columns s_i:
-  //  * segment pools (pairs [0, n_pairs_a)): one item per pixel = the block's samples of the
-  //    pixel; the lane traces them in the reference's s_i order (render.rs:185-189), keeps their
-  //    f64 running sum in LDS, then writes ONE f64 RGB partial per (pixel, s_j, block);
+  // one stratum row s_j (x one block of kPoolSi stratum columns s_i for segment and tail pools).
+  // Per pixel and s_j the samples are summed in the reference's s_i order (render.rs:185-189)
+  // as block partials p_b (a running sum over one block of kPoolSi samples, from 0) and the row
+  // total R = ((p_0 + p_1) + p_2) + ..., whoever computes them:
+  //  * row pools (pairs [0, n_pairs_r), non-BVH kernels): one item per pixel = all its samples
+  //    of the row; the lane keeps p_b and R in LDS and writes ONE f64 RGB value, R;
+  //  * segment pools (then up to n_pairs_a): one item per pixel = one block's samples; the lane
+  //    writes p_b and rt_reduce forms R;
   //  * tail pools (the last pairs): one item per pixel-sample, written as f64 RGB to its own
-  //    output value; rt_reduce sums a tail block's samples in s_i order, which is the running
-  //    sum a segment item computes, bit for bit. The tail keeps lanes busy while the last
-  //    segments finish, so the launch ends within a path or two per lane.
+  //    output value; rt_reduce forms p_b (the same running sum) and R.
+  // Row items keep the workspace at one value per (pixel, s_j); the segment band after them
+  // absorbs the rows' launch tail (a row is ~sqrt_spp paths) and the single-sample tail the
+  // segments' one, so the launch ends within a path or two per lane.
   // Idle lanes claim the next item of the wave's pool (ballot + mbcnt), across pool boundaries,
   // so lanes only idle at the very end of the launch. Wave-uniform pool state:
   const int lane = threadIdx.x & 63;
   int q = 0, si0 = 0, tx = 0, ty = 0, tile_w = 1, nv = 1, pool = 0, s_jp = 0;
   bool tailp = false;  // the pool is a tail pool (one item per sample)
+  bool rowp = false;   // the pool is a row pool (one item per pixel, every s_i)
+  uint32_t obase = 0;  // the pool's first output value (slot * 64)
   bool more = true;    // the queue may still hold pools
   constexpr uint32_t SC = Trav::kScene;  // the scene's material kinds and light-list shape
   const bool have_lights = (SC & kScLights) && P.n_lights > 0;
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
   constexpr int NB = BlockOf<BVH>::value;
-  // per-lane f64 running sum of the item in flight (segment items: the block's samples so far)
+  // per-lane f64 running sum of the item in flight (the block's samples so far), and of a row
+  // item the row total over its finished blocks (non-BVH kernels: the BVH kernels' LDS holds the
+  // compact trees, and they render no row items)
+  constexpr bool ROWS = !BVH;
   __shared__ double sh_acc[3 * NB];
+  __shared__ double sh_row[ROWS ? 3 * NB : 1];
   const int tid = threadIdx.x;
 
   d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
@@ -2121,13 +2135,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   bool alive = false;  // a path is in flight
   bool fresh = false;  // the lane's next sample needs its camera ray (claimed item / next s_i)
   uint32_t xk = 0;     // x | row-in-call << 16 | tail item << 31
-  uint32_t sij = 0;    // s_j << 16 | s_i of the sample in flight
+  uint32_t sij = 0;    // row item << 31 | s_j << 16 | s_i of the sample in flight
+  uint32_t oslot = 0;  // the item's output value (TraceParams::part: slot * 64 + pixel in tile)
   int next = 0;        // pool items claimed so far (wave-uniform)
   // a valid (non-zero) xoshiro state from the start: lanes without a path still run bounces on
   // stale rays at the end of a launch, and the rejection loops (random_unit_vector) must end
   Rng g = {0x9E3779B9u, 1u, 2u, 3u};
-  // A sample's radiance is final: add it to the item's running sum; a segment item continues
-  // with its next s_i, a finished item writes its f64 sum.
+  // A sample's radiance is final: add it to the item's running sum. Inside a block the item
+  // continues with its next s_i; at a block end a segment (or tail) item writes its f64 sum, a
+  // row item adds it to its row total and goes on, writing the total after its last block.
   auto end_sample = [&](d3 L) {
     // launch constants through the opaque kernarg pointer: read at the point of use instead of
     // being held in SGPRs across the path loop (kparams())
@@ -2140,18 +2156,24 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       sh_acc[tid] = a0, sh_acc[NB + tid] = a1, sh_acc[2 * NB + tid] = a2;
       sij += 1u;
       fresh = true;
-    } else {  // the item's output index (TraceParams::part), from its pixel and stratum
-      const int x = (int)(xk & 0xffffu), kr = (int)((xk >> 16) & 0x7fffu);
-      const int tx = x >> 3, tw = imin(kWaveTile, Q->W - tx * kWaveTile);
-      const uint32_t pv = (uint32_t)((kr & 7) * tw + (x & 7));
-      const uint32_t qq = (uint32_t)((kr >> 3) * Q->tiles_x + tx) * (uint32_t)Q->n_sj +
-                          ((sij >> 16) - (uint32_t)Q->sj0);
-      const uint32_t nb = (uint32_t)Q->n_blk, na = (uint32_t)Q->n_pairs_a;
-      const uint32_t outi =
-          (xk >> 31) ? (na * nb + (qq - na) * (uint32_t)Q->sqrt_spp + (sij & 0xffffu)) * 64u + pv
-                     : (qq * nb + (sij & 0xffffu) / (uint32_t)kPoolSi) * 64u + pv;
-      double* o = Q->part + (size_t)outi * 3;
-      o[0] = a0, o[1] = a1, o[2] = a2;
+    } else {
+      bool done = true;
+      if (ROWS && (sij >> 31)) {  // a row item's block ends: R = p_0, then R + p_b
+        if (s_n > kPoolSi) {
+          a0 = sh_row[tid] + a0, a1 = sh_row[NB + tid] + a1, a2 = sh_row[2 * NB + tid] + a2;
+        }
+        if (s_n < Q->sqrt_spp) {
+          sh_row[tid] = a0, sh_row[NB + tid] = a1, sh_row[2 * NB + tid] = a2;
+          sh_acc[tid] = 0.0, sh_acc[NB + tid] = 0.0, sh_acc[2 * NB + tid] = 0.0;
+          sij += 1u;
+          fresh = true;
+          done = false;
+        }
+      }
+      if (done) {
+        double* o = Q->part + (size_t)oslot * 3;
+        o[0] = a0, o[1] = a1, o[2] = a2;
+      }
     }
   };
 
@@ -2167,9 +2189,19 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       if (lane == 0) id = atomicAdd(Q->queue, 1u);
       id = __builtin_amdgcn_readfirstlane(id);
       if ((int)id < Q->n_pools) {
-        q = (int)id / Q->n_blk;
-        const int blk = (int)id - q * Q->n_blk;
+        const int r = ROWS ? Q->n_pairs_r : 0, nb = Q->n_blk;
+        int blk = 0;
+        rowp = ROWS && (int)id < r;
+        if (rowp) {
+          q = (int)id;
+        } else {
+          const int j = (int)id - r, m = j / nb;
+          blk = j - m * nb;
+          q = r + m;
+        }
         tailp = q >= Q->n_pairs_a;
+        obase = tailp ? (uint32_t)(r + (Q->n_pairs_a - r) * nb + (q - Q->n_pairs_a) * Q->sqrt_spp) * 64u
+                      : id * 64u;
         const int tile = q / Q->n_sj;
         tx = tile % Q->tiles_x;
         ty = tile / Q->tiles_x;
@@ -2209,7 +2241,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         const int x = tx * kWaveTile + cx;
         const int kr = ty * kWaveTile + cy;
         xk = (uint32_t)x | (uint32_t)kr << 16 | (tailp ? 0x80000000u : 0u);
-        sij = (uint32_t)s_jp << 16 | (uint32_t)s_i;
+        sij = (rowp ? 0x80000000u : 0u) | (uint32_t)s_jp << 16 | (uint32_t)s_i;
+        oslot = obase + (tailp ? (uint32_t)s_i * 64u : 0u) + (uint32_t)pv;
         sh_acc[tid] = 0.0, sh_acc[NB + tid] = 0.0, sh_acc[2 * NB + tid] = 0.0;
         fresh = true;
       }
@@ -2222,7 +2255,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" : "+v"(xk2));
       const int x = (int)(xk2 & 0xffffu);
       const int y = Q->row_begin + (int)((xk2 >> 16) & 0x7fffu) * Q->row_step;
-      const int s_i = (int)(sij & 0xffffu), s_j = (int)(sij >> 16);
+      const int s_i = (int)(sij & 0xffffu), s_j = (int)((sij >> 16) & 0x7fffu);
       Rng g2 = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
                         (uint32_t)(s_j * Q->sqrt_spp + s_i));
       d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
@@ -2237,7 +2270,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const kparams_t Q = kparams();
       const int x = (int)(xk & 0xffffu);
       const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
-      const int s_i = (int)(sij & 0xffffu), s_j = (int)(sij >> 16);
+      const int s_i = (int)(sij & 0xffffu), s_j = (int)((sij >> 16) & 0x7fffu);
       // get_ray render.rs:218-249 (stratum (s_i, s_j): 2 jitter draws, defocus disk, time)
       g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
                    (uint32_t)(s_j * Q->sqrt_spp + s_i));
@@ -2308,10 +2341,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       double t2;
       uint32_t hn2;
       int hf2;
-      traverse<true, COUNT, VOL, true, BVH>(P, P.root, ~0u, ro, rd, tm, ro, rd, -1, 0.0001 + z,
-                                            kInf, t2,
-                                      hn2, hf2, g, C);
-      asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2));
+      Rng g2 = g;  // the world query of this kernel (generated or interpreted), on a copy of g
+      d3 ro2 = ro;
+      ro2.x += z;
+      Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro2, rd, tm, t2, hn2, hf2, g2, C);
+      asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2), "v"(g2.s0));
     }
 #endif
     if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
@@ -2501,7 +2535,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       if (have_lights) {
         d3 p2 = p;
         asm volatile("" : "+v"(p2.x));
-        const double lp2 = light_pdf<COUNT>(P, p2, dir, cos_sl, C);
+        const double lp2 = Trav::template lights_pdf<COUNT>(P, p2, dir, cos_sl, C);
         asm volatile("" ::"v"(lp2));
       }
 #endif

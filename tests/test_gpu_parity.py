@@ -500,12 +500,17 @@ def _render_env(blob, cam, env, **kw):
 ])
 def test_chunked_and_tail_split_renders_are_bitwise_equal(gpu_available, name, kw):
     """The stratum-row chunk loop (RT_WORKSPACE_MB too small for one launch: several launches
-    carry the f64 running sums across rt_reduce calls) and the split between row items and
-    per-sample tail items (RT_TAIL_PAIRS) leave the image bit for bit unchanged."""
+    carry the f64 running sums across rt_reduce calls) and the split of a launch's (tile, s_j)
+    pairs into row items (the lane forms the row total), segment items (rt_reduce forms it from
+    block partials) and per-sample tail items (RT_SEG_PAIRS, RT_TAIL_PAIRS) leave the image bit
+    for bit unchanged. (BVH kernels render no row items: their splits are segment / tail.)"""
     blob, cam = rt.preset_blob(name, **kw)
     one = _render_env(blob, cam, {})
     for env in ({"RT_WORKSPACE_MB": 1}, {"RT_TAIL_PAIRS": 0}, {"RT_TAIL_PAIRS": 1 << 30},
-                {"RT_TAIL_PAIRS": 7, "RT_WORKSPACE_MB": 1}):
+                {"RT_TAIL_PAIRS": 7, "RT_WORKSPACE_MB": 1},
+                {"RT_SEG_PAIRS": 0, "RT_TAIL_PAIRS": 0}, {"RT_SEG_PAIRS": 0},
+                {"RT_SEG_PAIRS": 5, "RT_TAIL_PAIRS": 3},
+                {"RT_SEG_PAIRS": 0, "RT_TAIL_PAIRS": 0, "RT_WORKSPACE_MB": 1}):
         other = _render_env(blob, cam, env)
         assert np.array_equal(one, other, equal_nan=True), env
 
