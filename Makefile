@@ -63,8 +63,9 @@ VARIANTS := $(BUILD)/variants
 variants: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(VARIANTS)
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TRAV2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_trav2.so -lhiprtc
-	$(HIPCC) $(HIPFLAGS) -DRT_ABL_NOLPDF -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_nolpdf.so -lhiprtc
-	$(HIPCC) $(HIPFLAGS) -DRT_NO_QUADS -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_noquads.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_LPDF2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_lpdf2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_FRESH2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_fresh2.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_HIT2 -shared $(DEV_SRC) -o $(VARIANTS)/librtmi355x_abl_hit2.so -lhiprtc
 
 # occupancy variants of the BVH kernels; A/B with
 # VARDIR=build/variants_occ python tools_gpu/ab_variants.py W SPP ROUNDS SCENE

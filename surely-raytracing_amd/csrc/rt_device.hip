@@ -8,15 +8,18 @@
 // and Perlin noise (texture.rs:17-131, perlin.rs:30-96), vec3 math (vec3.rs).
 //
 // Work decomposition: persistent waves claim POOLS from a global queue; a pool
-// is one 8x8 pixel tile x one stratum row s_j x one block of kPoolSi stratum columns s_i. Each
-// lane traces one path at a time (ray_color's recursion -> an iterative bounce loop with beta/L)
-// and takes a segment item (one pixel's samples of the block, summed in f64 in LDS) or, for the
-// launch's last pools, one sample; when its item ends it writes the f64 partial and claims the
+// is one 8x8 pixel tile x one stratum row s_j (x one block of kPoolSi stratum columns s_i for
+// segment and tail pools). Each lane traces one path at a time (ray_color's recursion -> an
+// iterative bounce loop with beta/L) and takes a row item (all of one pixel's samples of the
+// row, summed per block and then per row in f64 in LDS), a segment item (one block) or, for the
+// launch's last pools, one sample; when its item ends it writes the f64 value and claims the
 // next item with a wave ballot + mbcnt, so lanes stay busy whatever the per-pixel path cost.
-// rt_reduce adds the f64 block partials in the reference's sample order (s_i inside s_j,
-// render.rs:185-189; the association differs from its single running sum only between blocks
-// of kPoolSi samples) into the caller's accumulator, so no atomics touch the framebuffer and results are bitwise
-// reproducible and identical across 1..8 GPUs (the RNG is keyed by global pixel and sample).
+// rt_reduce forms each row's total from block partials where a lane did not, and adds the rows
+// in the reference's sample order (s_i inside s_j, render.rs:185-189; the association differs
+// from its single running sum only between blocks and between rows) into the caller's
+// accumulator, so no atomics touch the framebuffer and results are bitwise reproducible and
+// identical across 1..8 GPUs and any split of the work (the RNG is keyed by global pixel and
+// sample).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
