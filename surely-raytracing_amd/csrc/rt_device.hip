@@ -461,9 +461,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     return set_err(RT_ERR_INVALID_ARG, "row range outside the image");
   if ((int64_t)W * cam->image_height >= (1ll << 32) || (int64_t)S * S >= (1ll << 32))
     return set_err(RT_ERR_UNSUPPORTED, "image or spp too large for 32-bit pixel/sample keys");
-  // lane item keys pack x (16 bits), the call's row index (15 bits) and s_j / s_i (16 bits each)
+  // lane item keys pack x (16 bits), the call's row index (15 bits), s_j (15 bits, beside the
+  // row-item bit) and s_i (16 bits)
   if (W > 65535 || opts->n_rows > 32767)
     return set_err(RT_ERR_UNSUPPORTED, "image_width > 65535 or n_rows > 32767 in one call");
+  if (S > 32768) return set_err(RT_ERR_UNSUPPORTED, "spp > 2^30 (sqrt_spp > 32768)");
   const int sj0 = opts->sj_count > 0 ? opts->sj_begin : 0;
   const int n_sj = opts->sj_count > 0 ? opts->sj_count : S;
   if (sj0 < 0 || sj0 + n_sj > S) return set_err(RT_ERR_INVALID_ARG, "bad stratum range");
@@ -711,12 +713,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   //  * Smaller launches (an N-way share, chunks) balance better without rows (C2 over 8 GPUs:
   //    0.940 of ideal with segments, 0.894 with half the pairs as rows, profiles/
   //    r03_scaling_probe_*.log): segment items, then a tail of one pair per resident wave.
-  //  * BVH kernels keep their LDS for the compact trees and render no rows. Row items need
-  //    s_j < 2^15 (lane key).
+  //  * BVH kernels keep their LDS for the compact trees and render no rows.
   // RT_SEG_PAIRS (rows with that band) and RT_TAIL_PAIRS override the sizes (tests: the image
   // does not depend on the split).
   const int64_t res_waves = max_blocks * (block / 64);
-  const bool rows_ok = !bvh && S < 32768;
+  const bool rows_ok = !bvh;
   const char* seg_env = std::getenv("RT_SEG_PAIRS");
   const char* tail_env = std::getenv("RT_TAIL_PAIRS");
   struct Split {
