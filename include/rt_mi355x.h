@@ -234,8 +234,9 @@ int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
 
 /* Asynchronous on `hip_stream` (hipStream_t, may be NULL): render into a DEVICE buffer.
  * If stats != NULL the call synchronises the stream to fill it. Limits: image_width <= 65535
- * (RT_ERR_UNSUPPORTED beyond); any number of rows (row ranges taller than 32760 rows run as
- * consecutive sub-renders, same image). rt_scene_destroy waits for the scene's renders. */
+ * and samples_per_pixel < 2^30 (sqrt_spp <= 32768; RT_ERR_UNSUPPORTED beyond); any number of
+ * rows (row ranges taller than 32760 rows run as consecutive sub-renders, same image).
+ * rt_scene_destroy waits for the scene's renders. */
 int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
                      float* accum_rgb_device, void* hip_stream, rt_stats* stats);
 
