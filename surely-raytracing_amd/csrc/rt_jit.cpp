@@ -86,7 +86,9 @@ struct Gen {
       rcp[k] = true;
     }
   }
-  // xform_in of the record at x (transform.rs:59, 86-107)
+  // xform_in of the record at x (transform.rs:59, 86-107). A translation leaves d, a rotation
+  // about y leaves d.y as they are (rt_kernel.h translate_in / rotate_y_in), so the reciprocals
+  // of those components stay valid.
   void xform(size_t x) {
     if ((N[x] & 0xffu) == RTL_TRANSLATE) {
       o << "    C.inc(RT_OP_TRANSLATE);\n    translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4))
@@ -94,8 +96,8 @@ struct Gen {
     } else {
       o << "    C.inc(RT_OP_ROTATE_Y);\n    rotate_y_in(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3))
         << ", o, d);\n";
+      rcp[0] = rcp[2] = false;
     }
-    frame_changed();
   }
   uint32_t code(size_t rec, int frame) {
     size_t id = 0;

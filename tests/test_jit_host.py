@@ -57,8 +57,10 @@ def test_cornell_walker_sequence():
     assert "(0x1.68p+6)" in src and "(0x1.09p+8), (0x0p+0), (0x1.27p+8)" in src
     lits = [float.fromhex(x) for x in re.findall(r"\((-?0x[0-9a-f.]+p[+-]\d+)\)", src)]
     assert all(struct.pack("<d", v) == struct.pack("<d", float.fromhex(v.hex())) for v in lits)
-    # rcp of each axis formed once per frame: 3 in the world frame, 3 in the box frame
-    assert len(re.findall(r"r[xyz] = rcp_nr1", world)) == 6
+    # rcp of each axis formed once per frame: 3 in the world frame, x and z in the box frame
+    # (RotateY leaves d.y as it is, the translation all of d)
+    assert len(re.findall(r"r[xyz] = rcp_nr1", world)) == 5
+    assert len(re.findall(r"ry = rcp_nr1", world)) == 1
     # the hit record's frame (transform.rs:57-135) for the box: the same chain with the same
     # literals, into the frame root first and back out innermost first; no interpreter fallback
     fin = src[src.index("void frame_in"):src.index("void frame_out")]
