@@ -98,6 +98,13 @@ variants-c4: $(DEV_SRC) $(DEV_HDR)
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_FRESH2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_fresh2.so -lhiprtc
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_HIT2 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_hit2.so -lhiprtc
 
+# upper bound of resumable top-level walks (wrong images): walks cut after K box steps
+variants-c4-budget: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(BUILD)/variants_c4b
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_BUDGET=6 -shared $(DEV_SRC) -o $(BUILD)/variants_c4b/librtmi355x_b06.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_BUDGET=10 -shared $(DEV_SRC) -o $(BUILD)/variants_c4b/librtmi355x_b10.so -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -DRT_ABL_BUDGET=14 -shared $(DEV_SRC) -o $(BUILD)/variants_c4b/librtmi355x_b14.so -lhiprtc
+
 variants-c4-walks: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)/variants_c4
 	$(HIPCC) $(HIPFLAGS) -DRT_ABL_TWICE_BVH=1 -shared $(DEV_SRC) -o $(BUILD)/variants_c4/librtmi355x_twice1.so -lhiprtc

@@ -1405,12 +1405,23 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   unsigned long long pf_leaf_cyc = 0;
   const unsigned long long pf_t0 = __builtin_readcyclecounter();
 #endif
+#ifdef RT_ABL_BUDGET  // ablation build (wrong images): a top-level walk stops after RT_ABL_BUDGET
+                      // box steps; the time is an upper bound for resumable walks
+  uint32_t ab_steps = 0;
+#endif
   for (;;) {
     // while-while: steps until the lane holds a leaf whose box was hit (or is done), then the
     // leaves with every lane that has one. (Postponing a lane's leaf and stepping on until every
     // lane holds one -- speculative while-while -- was 11 % slower at C4: more steps against an
     // older closest t.)
     while (ref < 0x8000u) {
+#ifdef RT_ABL_BUDGET
+      if (frame < 0 && ++ab_steps > RT_ABL_BUDGET) {
+        ref = kDone;
+        sp = 0;
+        break;
+      }
+#endif
       const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
       const uint32_t rr = refs[ref];
       float tn0, tn1;
