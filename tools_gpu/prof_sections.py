@@ -16,7 +16,7 @@ NAMES = ["pool/regen", "traverse", "hit record", "emit/metal/dielectric", "lambe
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell_box"
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 800
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 100
-lib = rt.load_device_lib("build/prof/librtmi355x.so")
+lib = rt.load_device_lib(os.environ.get("RT_PROF_LIB", "build/prof/librtmi355x.so"))
 blob, cam = rt.preset_blob(scene, width=W, spp=spp)
 h = C.c_void_p()
 assert lib.rt_scene_create(blob.ref(), 0, C.byref(h)) == 0, lib.rt_last_error()
