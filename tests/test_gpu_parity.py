@@ -515,6 +515,23 @@ def test_chunked_and_tail_split_renders_are_bitwise_equal(gpu_available, name, k
         assert np.array_equal(one, other, equal_nan=True), env
 
 
+def test_row_items_at_frame_scale_are_bitwise_equal(gpu_available):
+    """cornell_box at 800x800 and 256 spp (160 k (tile, s_j) pairs, enough for the default split
+    to render row items): the default split, segment items only, and row items
+    only (no band, no tail) give the same image bit for bit, and the default's workspace is one
+    value per (pixel, s_j) plus the band and the tail."""
+    blob, cam = rt.preset_blob("cornell_box", width=800, spp=256)
+    assert cam.sqrt_spp == 16
+    acc, st = _gpu(blob, cam)
+    per_value = 64 * 3 * 8  # one 64-pixel slot of f64 RGB
+    rows_only = 800 // 8 * 800 // 8 * cam.sqrt_spp * per_value
+    assert st.launches == 1 and rows_only < st.out_bytes < 2 * rows_only, st.out_bytes
+    for env in ({"RT_SEG_PAIRS": 1 << 30, "RT_TAIL_PAIRS": 4096},
+                {"RT_SEG_PAIRS": 0, "RT_TAIL_PAIRS": 0}):
+        other = _render_env(blob, cam, env)
+        assert np.array_equal(acc, other, equal_nan=True), env
+
+
 def test_bvh_walks_from_lds_global_and_reference_order_are_bitwise_equal(gpu_available):
     """final_scene at depth 40: the compact ordered BVHs walked from LDS (cbvh_walk, the product
     default), the per-octant ordered streams walked from global memory (RT_NO_CBVH_LDS) and the
