@@ -646,6 +646,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_NOISE2
   opts.push_back("-DRT_ABL_NOISE2");
 #endif
+#ifdef RT_ABL_RUV2
+  opts.push_back("-DRT_ABL_RUV2");
+#endif
 #ifdef RT_ABL_BUDGET
   opts.push_back("-DRT_ABL_BUDGET=" RTJ_STR(RT_ABL_BUDGET));
 #endif

@@ -2485,6 +2485,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const d3 un = uu;
       if (iso && !light_branch) {
         dir = random_unit_vector(g);  // SpherePDF::generate pdf.rs:51-53
+#ifdef RT_ABL_RUV2  // ablation build: the isotropic rejection loop run twice on a copy of the
+                    // RNG (same image; its cost)
+        {
+          Rng g2 = g;
+          asm volatile("" : "+v"(g2.s0));
+          const d3 d2 = random_unit_vector(g2);
+          asm volatile("" ::"v"(d2.x), "v"(g2.s1));
+        }
+#endif
       } else if ((SC & kScLOther) && light_branch && ltype != RTL_QUAD && ltype != RTL_SPHERE) {
         dir = mk(1., 0., 0.);  // Object::random default arm (object.rs:300)
       } else {
