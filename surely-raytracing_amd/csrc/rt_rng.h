@@ -49,8 +49,12 @@ __device__ __forceinline__ uint32_t rng_u32(Rng& g) {
 }
 // random_double (utils.rs:5-7): 32-bit uniform in [0, 1), exact in f64
 __device__ __forceinline__ double rnd(Rng& g) { return (double)rng_u32(g) * 0x1p-32; }
-// random_range(-1, 1) (utils.rs:9-11)
-__device__ __forceinline__ double rnd_pm1(Rng& g) { return -1.0 + 2.0 * rnd(g); }
+// random_range(-1, 1) (utils.rs:9-11): -1 + 2 * (u * 2^-32) = u * 2^-31 - 1, every step exact
+// (u has 32 significant bits, the sum at most 33), so one fma gives the same bits as the
+// reference's two operations (the oracle computes them as written)
+__device__ __forceinline__ double rnd_pm1(Rng& g) {
+  return __builtin_fma((double)rng_u32(g), 0x1p-31, -1.0);
+}
 // random_int(0, n-1) (utils.rs:13-15): multiply-high
 __device__ __forceinline__ uint32_t rnd_index(Rng& g, uint32_t n) { return __umulhi(rng_u32(g), n); }
 
