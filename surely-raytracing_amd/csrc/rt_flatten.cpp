@@ -14,6 +14,8 @@
 #include <cstring>
 #include <memory>
 
+#include <xmmintrin.h>
+
 namespace rtf {
 
 namespace {
@@ -47,6 +49,64 @@ struct Reader {
     err = true;
   }
 };
+
+// The axis-aligned quad test's planar coordinate is a(y) = fl(fl(y - q) * c), with y the hit
+// point's coordinate along u or v, and it accepts when !(a < 0) & !(1 < a) (NaN accepts,
+// object.rs:473). For finite q and finite c != 0, a(y) is monotone in y (both roundings are), so
+// the accepted finite y form one interval [lo, hi] of doubles and the device compares y with
+// those two bounds instead of forming a (rt_layout.h). lo/hi are found by bisection over the
+// doubles' order; false (keep the general test) for any other q, c.
+bool accept_interval(double q, double c, double& lo, double& hi) {
+  if (!std::isfinite(q) || !std::isfinite(c) || c == 0.0) return false;
+  // the device arithmetic: IEEE f64, round to nearest, no flush of subnormals (whatever the
+  // calling process set in MXCSR)
+  struct Csr {
+    unsigned v = _mm_getcsr();
+    Csr() { _mm_setcsr(v & ~0x8040u); }  // FTZ, DAZ off
+    ~Csr() { _mm_setcsr(v); }
+  } csr;
+  auto a_of = [&](double y) {
+    volatile double x = y - q;
+    volatile double a = x * c;
+    return (double)a;
+  };
+  auto key = [](double v) {  // order-preserving integer key (+0 and -0 share 0)
+    int64_t b;
+    std::memcpy(&b, &v, 8);
+    return b >= 0 ? b : INT64_MIN - b;
+  };
+  auto val = [](int64_t k) {
+    const int64_t b = k >= 0 ? k : INT64_MIN - k;
+    double v;
+    std::memcpy(&v, &b, 8);
+    return v;
+  };
+  const int64_t kmin = key(-HUGE_VAL), kmax = key(HUGE_VAL);
+  // the first key where a predicate that is monotone over [kmin, kmax] turns true (kmax + 1: never)
+  auto first_true = [&](auto pred) {
+    int64_t l = kmin, h = kmax + 1;
+    while (l < h) {
+      const int64_t m = l + (h - l) / 2;
+      if (pred(val(m))) h = m; else l = m + 1;
+    }
+    return h;
+  };
+  int64_t klo, khi;
+  if (c > 0.0) {  // a non-decreasing: a >= 0 from klo on, a <= 1 up to khi
+    klo = first_true([&](double y) { return !(a_of(y) < 0.0); });
+    khi = first_true([&](double y) { return 1.0 < a_of(y); }) - 1;
+  } else {        // a non-increasing: a <= 1 from klo on, a >= 0 up to khi
+    klo = first_true([&](double y) { return !(1.0 < a_of(y)); });
+    khi = first_true([&](double y) { return a_of(y) < 0.0; }) - 1;
+  }
+  // y = q gives a = 0, so the interval holds q and its bounds are finite
+  if (!(klo <= key(q) && key(q) <= khi) || klo <= kmin || khi >= kmax) return false;
+  lo = val(klo);
+  hi = val(khi);
+  // the bounds and their neighbours outside, checked directly against the predicate
+  auto acc = [&](double y) { const double a = a_of(y); return !(a < 0.0) && !(1.0 < a); };
+  return acc(lo) && acc(hi) && !acc(val(klo - 1)) && !acc(val(khi + 1));
+}
 
 std::unique_ptr<Node> read_node(Reader& r, int depth) {
   if (depth > 256) {
@@ -252,14 +312,17 @@ struct Emitter {
     if (!(nk == 1.0 || nk == -1.0) || f[9 + i] != 0.0 || f[9 + j] != 0.0) return;
     if (f[15] != nk * f[k]) return;  // D = n.q = n_k q_k
     if (single(A) != i || single(B) != j) return;
+    // a = (y_i - q_i) A_i and b = (y_j - q_j) B_j accept exactly on intervals of y_i and y_j
+    double lo_i, hi_i, lo_j, hi_j;
+    if (!accept_interval(f[i], A[i], lo_i, hi_i) || !accept_interval(f[j], B[j], lo_j, hi_j)) return;
     w[p] |= (uint32_t)(k + 1) << 8;
     putd(w, p, ax + 0, f[k]);
     if (i < j) {
-      putd(w, p, ax + 1, f[i]), putd(w, p, ax + 2, A[i]), putd(w, p, ax + 3, f[j]);
-      putd(w, p, ax + 4, B[j]);
+      putd(w, p, ax + 1, lo_i), putd(w, p, ax + 2, hi_i), putd(w, p, ax + 3, lo_j);
+      putd(w, p, ax + 4, hi_j);
     } else {
-      putd(w, p, ax + 1, f[j]), putd(w, p, ax + 2, B[j]), putd(w, p, ax + 3, f[i]);
-      putd(w, p, ax + 4, A[i]);
+      putd(w, p, ax + 1, lo_j), putd(w, p, ax + 2, hi_j), putd(w, p, ax + 3, lo_i);
+      putd(w, p, ax + 4, hi_i);
     }
   }
   void sphere(const Node& n, bool light) {

@@ -192,10 +192,9 @@ bool gen_volume_two_hits(const std::vector<uint32_t>& N, size_t node, std::ostri
       b << "    {\n      const AQuad q = {" << N[q] << "u, " << lit(pd(N, q, 0)) << ", "
         << lit(pd(N, q, 1)) << ", " << lit(pd(N, q, 2)) << ", " << lit(pd(N, q, 3)) << ", "
         << lit(pd(N, q, 4)) << "};\n"
-        << "      double t, a, b;\n      aquad_core<" << K << ">(q, o, d, r, t, a, b);\n"
+        << "      double t;\n      bool inr;\n      aquad_core<" << K << ">(q, o, d, r, t, inr);\n"
         << "      const double dk = d." << ax[K] << ";\n"
-           "      const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);\n"
-           "      const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);\n"
+           "      const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & inr;\n"
            "      const double te = v ? t : kInf;\n"
            "      m2 = __builtin_fmin(m2, __builtin_fmax(m1, te));\n"
            "      m1 = __builtin_fmin(m1, te);\n    }\n";

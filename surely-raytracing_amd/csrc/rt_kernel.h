@@ -466,7 +466,8 @@ __device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double
   double b = dot(pq, ld3(q, 12));
   const bool plane = !(fabs(denom) < 1e-8);
   const bool range = plane & (tmin <= t) & (t <= tmax);
-  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);  // as in aquad_test
+  // IEEE minNum/maxNum: a NaN coordinate drops out, and the reference's comparisons accept it
+  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
   const bool hit = range & !(lo < 0.0) & !(1.0 < hi);
   C.inc_if(RT_OP_QUAD_PLANE, plane);
   C.inc_if(RT_OP_QUAD_INTERVAL, range);
@@ -486,40 +487,40 @@ __device__ __forceinline__ double hilo(uint32_t lo, uint32_t hi) {
 }
 struct AQuad {  // the first 64 bytes of a world QUAD record
   uint32_t h0;
-  double qk, qlo, clo, qhi, chi;
+  double qk, lo0, lo1, hi0, hi1;  // accepted hit-point coordinates per in-plane axis (rt_layout.h)
 };
 template <class Ptr>
 __device__ __forceinline__ AQuad load_aquad(Ptr Q) {
   const uint4 a = ld4u(Q), b = ld4u(Q + 4), c = ld4u(Q + 8), e = ld4u(Q + 12);
   return {a.x, hilo(b.x, b.y), hilo(b.z, b.w), hilo(c.x, c.y), hilo(c.z, c.w), hilo(e.x, e.y)};
 }
-// t and the planar coordinates of an axis-aligned quad (shared by the test below and the
-// one-walk ConstantMedium boundary)
+// t of an axis-aligned quad and whether its planar coordinates a, b lie in [0, 1] (shared by
+// the test below and the one-walk ConstantMedium boundary). a = fl(fl(y - q) C) is monotone in
+// the hit point's coordinate y, so the accept test !(a < 0) & !(1 < a) (NaN accepts, object.rs:473)
+// is y in the record's [y0, y1] or NaN, compared directly (rt_layout.h; four compares instead of
+// two subtractions, two products, min/max and two compares).
 template <int K>
-__device__ __forceinline__ void aquad_core(const AQuad& q, d3 o, d3 d, d3 r, double& t, double& a,
-                                           double& b) {
+__device__ __forceinline__ void aquad_core(const AQuad& q, d3 o, d3 d, d3 r, double& t, bool& inr) {
   constexpr int LO = K == 0 ? 1 : 0, HI = K == 2 ? 1 : 2;
   const double dk = comp<K>(d), rk = comp<K>(r);
   const double num = q.qk - comp<K>(o);
   const double t0 = num * rk;
   t = fma(fma(-dk, t0, num), rk, t0);  // div_nr(num, dk)
-  a = (fma(t, comp<LO>(d), comp<LO>(o)) - q.qlo) * q.clo;
-  b = (fma(t, comp<HI>(d), comp<HI>(o)) - q.qhi) * q.chi;
+  const double ya = fma(t, comp<LO>(d), comp<LO>(o)), yb = fma(t, comp<HI>(d), comp<HI>(o));
+  inr = !(ya < q.lo0) & !(q.lo1 < ya) & !(yb < q.hi0) & !(q.hi1 < yb);
 }
 template <bool COUNT, int K>
 __device__ __forceinline__ bool aquad_test(const AQuad& q, d3 o, d3 d, d3 r, double tmin,
                                            double tmax, double& t_out, Ctr<COUNT>& C) {
   C.inc(RT_OP_QUAD_TESTS);
   const double dk = comp<K>(d);
-  double t, a, b;
-  aquad_core<K>(q, o, d, r, t, a, b);
-  // straight-line predicate. a, b in [0, 1] as min/max (IEEE minNum/maxNum): min(a, b) < 0 or
-  // 1 < max(a, b) exactly when the reference rejects (object.rs:473), NaN included (a NaN
-  // coordinate drops out of min/max, and the reference's comparisons accept it too)
+  double t;
+  bool inr;
+  aquad_core<K>(q, o, d, r, t, inr);
+  // straight-line predicate
   const bool plane = !(fabs(dk) < 1e-8);
   const bool range = plane & (tmin <= t) & (t <= tmax);
-  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
-  const bool hit = range & !(lo < 0.0) & !(1.0 < hi);
+  const bool hit = range & inr;
   C.inc_if(RT_OP_QUAD_PLANE, plane);
   C.inc_if(RT_OP_QUAD_INTERVAL, range);
   C.inc_if(RT_OP_QUAD_HITS, hit);
@@ -748,16 +749,16 @@ __device__ bool volume_two_hits(const TraceParams& P, uint32_t node, uint32_t ki
   double m1 = kInf, m2 = kInf;
   for (uint32_t k = 0; k < cnt; ++k, Q += RTL_QUAD_WORDS) {
     const AQuad q = load_aquad(Q);
-    double t, a, b;
+    double t;
     double dk;
+    bool inr;
     switch (RTL_QUAD_AXIS(q.h0)) {
-      case 1u: aquad_core<0>(q, o, d, r, t, a, b); dk = d.x; break;
-      case 2u: aquad_core<1>(q, o, d, r, t, a, b); dk = d.y; break;
-      default: aquad_core<2>(q, o, d, r, t, a, b); dk = d.z; break;
+      case 1u: aquad_core<0>(q, o, d, r, t, inr); dk = d.x; break;
+      case 2u: aquad_core<1>(q, o, d, r, t, inr); dk = d.y; break;
+      default: aquad_core<2>(q, o, d, r, t, inr); dk = d.z; break;
     }
-    const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
     // aquad_test's predicate without the interval, plus t >= -inf (not NaN)
-    const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & !(lo < 0.0) & !(1.0 < hi);
+    const bool v = !(fabs(dk) < 1e-8) & (-kInf <= t) & inr;
     const double te = v ? t : kInf;
     m2 = __builtin_fmin(m2, __builtin_fmax(m1, te));
     m1 = __builtin_fmin(m1, te);
@@ -1187,15 +1188,16 @@ __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d
       const AQuad q = qn;
       qn = load_aquad(Q + RTL_QUAD_WORDS);
       const uint32_t axis = RTL_QUAD_AXIS(q.h0);
-      double t, a, b, dk;
+      double t, dk;
+      bool inr;
       if (axis == 1u) {
-        aquad_core<0>(q, o, d, r, t, a, b);
+        aquad_core<0>(q, o, d, r, t, inr);
         dk = d.x;
       } else if (axis == 2u) {
-        aquad_core<1>(q, o, d, r, t, a, b);
+        aquad_core<1>(q, o, d, r, t, inr);
         dk = d.y;
       } else if (axis == 3u) {
-        aquad_core<2>(q, o, d, r, t, a, b);
+        aquad_core<2>(q, o, d, r, t, inr);
         dk = d.z;
       } else {  // quad_test's arithmetic (object.rs:453-490)
         const gptr G = Q + RTL_QUAD_GEN;
@@ -1203,11 +1205,11 @@ __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d
         dk = dot(n, d);
         t = div_nr(ldd(G, 3) - dot(n, o), dk);
         const d3 pq = vfma(t, d, o) - ld3(G, 4);
-        a = dot(pq, ld3(G, 8));
-        b = dot(pq, ld3(G, 12));
+        const double a = dot(pq, ld3(G, 8)), b = dot(pq, ld3(G, 12));
+        const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+        inr = !(lo < 0.0) & !(1.0 < hi);
       }
-      const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
-      cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & !(lo < 0.0) & !(1.0 < hi), t, qrec);
+      cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & inr, t, qrec);
     }
   }
 }

@@ -59,14 +59,17 @@
  * (object.rs:503-506). */
 /* World QUAD records (48 words) put an axis-aligned form FIRST, so one 64-byte scalar load
  * covers the header and everything the axis-aligned test reads, and the general payload after it:
- *   [hdr | axis << 8][skip][mat][next] d0-5 q_k, q_lo, C_lo, q_hi, C_hi, 0 | d6-21 general payload
+ *   [hdr | axis << 8][skip][mat][next] d0-5 q_k, y0_lo, y1_lo, y0_hi, y1_hi, 0 | d6-21 general payload
  * (the QUAD layout above, read through X + RTL_QUAD_GEN). axis = k + 1 when the quad is
  * axis-aligned in its frame (u along axis i, v along axis j, normal along k; 0 = general). Then
  * n = +-e_k, D = +-q_k, and A, B each have one non-zero component, so the general test's
  *   t = (D - n.o) / (n.d) = (q_k - o_k) / d_k,   a = pq.A = pq_i A_i,   b = pq.B = pq_j B_j
- * hold bit for bit (the dropped terms are exact zeros). lo/hi = the in-plane axes in ascending
- * order, (q, C) = (q_i, A_i) or (q_j, B_j) accordingly: the accept test on (a, b) is symmetric,
- * so only k varies per record. rt_flatten.cpp verifies the zero pattern before setting it. */
+ * hold bit for bit (the dropped terms are exact zeros), with pq_i = y_i - q_i, y = o + t d.
+ * a = fl(fl(y_i - q_i) A_i) is monotone in y_i, so "a in [0, 1] or NaN" is "y_i in [y0, y1] or
+ * NaN" for two doubles the flattener finds by bisection (rt_flatten.cpp accept_interval): the
+ * device compares y with them instead of forming a and b. lo/hi = the in-plane axes in ascending
+ * order: the accept test on (a, b) is symmetric, so only k varies per record. rt_flatten.cpp
+ * verifies the zero pattern (and finite, non-zero q, C) before setting the form. */
 #define RTL_QUAD_GEN 12
 #define RTL_QUAD_WORDS 48
 #define RTL_QUAD_AXIS(h) (((h) >> 8) & 0x3u)
