@@ -1371,8 +1371,14 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   constexpr float kBoxRel = 0x1p-20f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
-  const f32x2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
+  // slab times as fma(bound, inv, -o inv): one packed fma per axis instead of a subtraction and
+  // a product. The extra rounding of o inv is 2^-24 |o inv| <= 2^-24 (|bound| + |bound - o|) |inv|,
+  // the same two parts as o's own rounding (obvh_walk's budget): inside the bounds' margin and
+  // relative to t. A NaN slab time (0 * inf, inf - inf: d_a = 0) constrains nothing (fmaxf /
+  // fminf drop it), so such boxes are kept, never dropped.
   const f32x2 ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
+  const f32x2 nox2 = {-(ox * ix), -(ox * ix)}, noy2 = {-(oy * iy), -(oy * iy)},
+              noz2 = {-(oz * iz), -(oz * iz)};
   const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
   double closest = tmax;
   float close_f = (float)(closest + closest * (2.0 * kTieRel));
@@ -1391,7 +1397,9 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   // is hi where d_a < 0, as in the OBVH streams
   auto box = [&](float lx, float hx, float ly, float hy, float lz, float hz, float& tn) {
     const f32x2 bx = {lx, hx}, by = {ly, hy}, bz = {lz, hz};
-    const f32x2 tx2 = (bx - ox2) * ix2, ty2 = (by - oy2) * iy2, tz2 = (bz - oz2) * iz2;
+    const f32x2 tx2 = __builtin_elementwise_fma(bx, ix2, nox2),
+                ty2 = __builtin_elementwise_fma(by, iy2, noy2),
+                tz2 = __builtin_elementwise_fma(bz, iz2, noz2);
     const float tnx = nx ? tx2.y : tx2.x, tfx = nx ? tx2.x : tx2.y;
     const float tny = ny ? ty2.y : ty2.x, tfy = ny ? ty2.x : ty2.y;
     const float tnz = nz ? tz2.y : tz2.x, tfz = nz ? tz2.x : tz2.y;
