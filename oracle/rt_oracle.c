@@ -9,7 +9,8 @@
  * and is unseeded (rand::thread_rng, utils.rs:5-15), so no golden pixel vectors exist upstream.
  * This restatement is pinned by (a) analytic known-answer tests derived from the reference
  * formulas (tests/test_oracle_kat.py) and (b) statistics of the reference's own renders
- * final_images/book3.png and mixed_pdf.png (tests/golden/final_images_stats.json).
+ * final_images/{book3,mixed_pdf,cornell_smoke,book2}.png (tests/golden/final_images_stats.json,
+ * tests/test_oracle_render.py).
  *
  * Structure follows the reference function by function, RECURSIVELY (not the threaded GPU
  * traversal), so that it independently checks the device's flattening:
@@ -24,14 +25,18 @@
  *   textures           texture.rs:17-131      Perlin perlin.rs:30-96 RtImage::pixel_data rt_image.rs:37-46
  *
  * Two builds (ORACLE_F64 = 0/1):
- *   f32: the GPU-parity restatement. Geometry/sampling arithmetic follows the fp32 operation
- *        spec in DESIGN.md §4 (explicit fma, correctly rounded / and sqrt, polynomial
- *        transcendentals below), so every path decision matches the device bit for bit.
- *   f64: reference precision (the reference is all f64), libm transcendentals, plain a*b+c.
- *        Used as the CPU baseline ("port") and as a precision cross-check.
+ *   f64: the parity oracle. Reference precision (the reference is all f64) and the reference's
+ *        own operation order, expression by expression: no contraction (-ffp-contract=off), the
+ *        association Rust's left-to-right evaluation gives (a*u + b*v) + c*w, IEEE / and sqrt
+ *        where the reference divides or takes a root, libm transcendentals. Also the CPU
+ *        baseline ("port") of bench.py.
+ *   f32: a precision study only (tests/test_oracle_render.py shows why the device is f64):
+ *        the same algorithm in float, with fma and polynomial transcendentals.
+ * Deliberate deviations from the reference's arithmetic: the RNG (SURVEY App. A
+ * S4: a seeded counter stream instead of unseeded ChaCha12, 32-bit uniforms) and the semantics
+ * register S1-S3 (S1 empty lights -> material PDF alone; S2 Isotropic scattering_pdf =
+ * 1/(4pi); RT_FLAG_SEMANTICS_REFERENCE restores the reference behaviour); nothing else.
  * Both builds draw the same per-sample RNG stream.
- * Semantics register: S1 empty lights -> material PDF alone; S2 Isotropic
- * scattering_pdf = 1/(4pi); RT_FLAG_SEMANTICS_REFERENCE restores the reference behaviour.
  */
 #include <math.h>
 #include <pthread.h>
@@ -187,7 +192,6 @@ static void sincos2pi(double u, double* s, double* c) {
   *s = sin(phi);
   *c = cos(phi);
 }
-#define INV_PI (1.0 / PI_D)
 #else
 #define LOG f32_log
 #define POW powf
@@ -195,7 +199,6 @@ static void sincos2pi(double u, double* s, double* c) {
 #define ACOS f32_acos
 #define ATAN2 f32_atan2
 #define sincos2pi f32_sincos2pi
-#define INV_PI 0x1.45f306p-2f
 #endif
 
 /* =============================================================== RNG
@@ -296,7 +299,7 @@ static inline vec3 ray_at(const ray_t* r, real t) { return vfma(t, r->d, r->o); 
 typedef struct {
   int tag, mat, moving;
   vec3 c, cv;
-  real radius, inv_radius;
+  real radius;
   vec3 q, u, v, n, w;
   real d, area;
   vec3 off;
@@ -396,7 +399,6 @@ static int parse_obj(oscene* sc, cursor* c, int depth) {
       tmp.moving = (int)ci(c);
       tmp.c = cv3(c);
       tmp.radius = R(cf(c));
-      tmp.inv_radius = R(1) / tmp.radius;
       tmp.cv = cv3(c);
       read_bbox(c, &tmp);
       sc->nodes[id] = tmp;
@@ -607,7 +609,9 @@ static int sphere_hit(ctx_t* cx, const onode* s, int node, const ray_t* r, real 
   CNT(cx, RT_OP_SPHERE_HITS);
   rec->t = root;
   rec->p = ray_at(r, root);
-  vec3 outward = vscale(vsub(rec->p, center), s->inv_radius);
+  /* (p - center) / radius, component by component (object.rs:169, Div<f64> vec3.rs:152-154) */
+  vec3 pc = vsub(rec->p, center);
+  vec3 outward = v3(pc.x / s->radius, pc.y / s->radius, pc.z / s->radius);
   rec->outward_local = outward;
   rec->u = R(0);
   rec->v = R(0);
@@ -826,8 +830,8 @@ static onb_t onb_from_w(vec3 w) { /* onb.rs:32-47 */
   b.w = unit_w;
   return b;
 }
-static vec3 onb_local(const onb_t* b, vec3 a) { /* onb.rs:24-26 */
-  return vfma(a.x, b->u, vfma(a.y, b->v, vscale(b->w, a.z)));
+static vec3 onb_local(const onb_t* b, vec3 a) { /* onb.rs:24-26: (a*u + b*v) + c*w */
+  return vadd(vadd(vscale(b->u, a.x), vscale(b->v, a.y)), vscale(b->w, a.z));
 }
 static vec3 random_cosine_direction(rng_t* g) { /* vec3.rs:240-250 */
   real r1 = rnd(g), r2 = rnd(g);
@@ -987,8 +991,8 @@ static vec3 ray_color(ctx_t* cx, const camctx* cc, const ray_t* r, int depth, rn
   if (iso) {
     mat_pdf = R(1.0 / (4.0 * PI_D)); /* SpherePDF::value pdf.rs:47-49 */
   } else {
-    real cth = dot(udir, uvw.w); /* CosinePDF::value pdf.rs:69-73 */
-    real v = cth * INV_PI;
+    real cth = dot(udir, uvw.w); /* CosinePDF::value pdf.rs:69-73: max(0, cos / PI) */
+    real v = cth / R(PI_D);
     mat_pdf = v > R(0) ? v : R(0);
   }
   if (have_lights) {
@@ -1002,7 +1006,7 @@ static vec3 ray_color(ctx_t* cx, const camctx* cc, const ray_t* r, int depth, rn
     s_pdf = (cx->flags & RT_FLAG_SEMANTICS_REFERENCE) ? R(0) : R(1.0 / (4.0 * PI_D));
   } else {
     real cth = dot(rec.normal, udir); /* Lambertian::scattering_pdf material.rs:100-108 */
-    s_pdf = cth < R(0) ? R(0) : cth * INV_PI;
+    s_pdf = cth < R(0) ? R(0) : cth / R(PI_D);
   }
   ray_t sr = {rec.p, dir, r->tm};
   vec3 L = ray_color(cx, cc, &sr, depth - 1, g);

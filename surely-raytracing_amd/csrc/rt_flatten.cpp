@@ -333,7 +333,7 @@ struct Emitter {
     if (n.moving) w[p] |= RTL_SPHERE_MOVING;
     putd(w, p, 0, f[0]), putd(w, p, 1, f[1]), putd(w, p, 2, f[2]), putd(w, p, 3, f[3]);
     putd(w, p, 4, f[4]), putd(w, p, 5, f[5]), putd(w, p, 6, f[6]);
-    putd(w, p, 7, 1.0 / f[3]);  // outward = (p - c) * (1/r)
+    putd(w, p, 7, 1.0 / f[3]);  // IEEE 1/r: outward = (p - c) / r by one residual step (rt_kernel.h)
     if (!light) {  // c +- r, and at c + cvec when moving (object.rs:88-105)
       PrimBox b;
       const double r = std::fabs(f[3]);

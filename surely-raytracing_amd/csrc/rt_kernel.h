@@ -1848,8 +1848,10 @@ __device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {
 struct Onb {
   d3 u, v, w;
 };
-__device__ __forceinline__ d3 onb_local(const Onb& b, d3 a) {  // onb.rs:24-26
-  return vfma(a.x, b.u, vfma(a.y, b.v, b.w * a.z));
+// onb.rs:24-26 evaluates a*u + b*v + c*w left to right, (a*u + b*v) + c*w: the same association
+// here, each sum fused with its product
+__device__ __forceinline__ d3 onb_local(const Onb& b, d3 a) {
+  return vfma(a.z, b.w, vfma(a.x, b.u, b.v * a.y));
 }
 __device__ __forceinline__ d3 random_cosine_direction(Rng& g) {  // vec3.rs:240-250
   double r1 = rnd(g);
@@ -2411,7 +2413,14 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     } else if (type == RTL_SPHERE) {
       d3 c = ld3(X, 0);
       if (X[0] & RTL_SPHERE_MOVING) c = vfma(tm, ld3(X, 4), c);
-      outward = (p - c) * ldd(X, 7);
+      // (p - c) / radius (object.rs:169): q = x (1/r) with the host's IEEE reciprocal, then one
+      // residual step q + fma(-q, r, x) (1/r), which is the correctly rounded quotient
+      // (Markstein: 1/r correctly rounded, q within an ulp), i.e. the reference's division
+      const d3 pc = p - c;
+      const double ir = ldd(X, 7), rad = ldd(X, 3);
+      const d3 q0 = pc * ir;
+      outward = mk(fma(fma(-q0.x, rad, pc.x), ir, q0.x), fma(fma(-q0.y, rad, pc.y), ir, q0.y),
+                   fma(fma(-q0.z, rad, pc.z), ir, q0.z));
       if (needs_uv) sphere_uv(outward, u, v);
     } else {
       outward = mk(1., 0., 0.);

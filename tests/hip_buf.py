@@ -21,7 +21,30 @@ def hip() -> C.CDLL:
         _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         _hip.hipSetDevice.argtypes = [C.c_int]
         _hip.hipDeviceSynchronize.argtypes = []
+        _hip.hipStreamCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+        _hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+        _hip.hipStreamDestroy.argtypes = [C.c_void_p]
     return _hip
+
+
+class Stream:
+    """A non-blocking HIP stream on `device` (hipStreamCreateWithFlags)."""
+
+    def __init__(self, device: int = 0):
+        h = hip()
+        assert h.hipSetDevice(device) == 0
+        s = C.c_void_p()
+        assert h.hipStreamCreateWithFlags(C.byref(s), 1) == 0  # hipStreamNonBlocking
+        self.handle = s.value
+
+    def sync(self):
+        assert hip().hipStreamSynchronize(C.c_void_p(self.handle)) == 0
+
+    def destroy(self):
+        if self.handle:
+            self.sync()
+            hip().hipStreamDestroy(C.c_void_p(self.handle))
+            self.handle = None
 
 
 class DevBuf:
