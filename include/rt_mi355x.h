@@ -188,8 +188,9 @@ typedef struct rt_stats {
   double ms_total;   /* host wall time of the call                                  */
   uint64_t samples;  /* pixel-samples rendered by this call                         */
   uint64_t ops[32];  /* rt_op_counter values (RT_FLAG_COUNT_OPS only)               */
-  uint64_t out_bytes; /* f64 partial / tail-sample bytes the path kernel stored (and   */
-                      /* rt_reduce read back): the algorithmic HBM bytes of the render  */
+  uint64_t out_bytes; /* f64 workspace bytes the path kernel stored (row totals, block   */
+                      /* partials, tail samples) and rt_reduce read back: a design choice, */
+                      /* not the path's algorithmic bytes (the W*H*12 B f32 framebuffer)   */
   uint32_t launches;  /* path-kernel launches (stratum-row chunks) of the render        */
   uint32_t _pad0;
 } rt_stats;
@@ -217,7 +218,8 @@ void rt_scene_destroy(rt_scene* scene);
 /* Bytes of the device-side flattened scene (nodes + materials + textures + tables). */
 uint64_t rt_scene_device_bytes(const rt_scene* scene);
 /* Scene-specialised product kernel (the world walker generated from the scene and compiled by
- * hiprtc on the first product render; BVH scenes use the interpreter walkers).
+ * hiprtc on the first product render; a BVH subtree record calls the per-lane BVH walk from the
+ * generated walker, so BVH scenes such as final_scene run it too).
  * *state: 1 compiled and in use, 0 not compiled yet, -1 not generated for this scene (or
  * RT_JIT=0), -2 compilation failed (the interpreter kernel runs). msg: the reason or the log. */
 int rt_scene_jit_info(rt_scene* scene, int* state, char* msg, uint32_t msg_len);
@@ -227,6 +229,15 @@ int rt_scene_jit_info(rt_scene* scene, int* state, char* msg, uint32_t msg_len);
  * status when compilation fails (msg receives the log). */
 int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* msg,
                  uint32_t msg_len);
+
+/* Re-entrancy (render_par_lights takes &HittableList and may run concurrently, render.rs:144-150):
+ * renders of ONE scene may be issued from several host threads and on several streams at once,
+ * each into its own output buffer. Every render call takes a private slot of per-render state
+ * (pool-queue word, op counters, f64 workspace, events): a slot whose previous render has
+ * finished or went to the same stream, else a new one (up to 8 per scene; beyond that a call
+ * waits for a slot to finish). Renders on different streams therefore run concurrently and each
+ * gives its serial image bit for bit. Two renders into the SAME output buffer are ordered only by
+ * the caller (same stream, or events). rt_scene_destroy must not race with renders of the scene. */
 
 /* Synchronous: render into a HOST buffer (n_rows * W * 3 floats). */
 int rt_render(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts, float* accum_rgb,
@@ -247,8 +258,8 @@ int rt_render_device(rt_scene* scene, const rt_camera* cam, const rt_render_opts
 #define RT_TRACE_HISTORY 64
 int rt_scene_trace_ms(rt_scene* scene, float* ms_out, int max_n, int* n_out);
 
-/* Diagnostics: counters of a profiling build of the library (-DRT_PROF, tools_gpu/); zeros in
- * the product build. */
+/* Diagnostics: counters of a profiling build of the library (-DRT_PROF, tools_gpu/) from the
+ * scene's latest render; zeros in the product build. */
 int rt_scene_prof_counters(rt_scene* scene, uint64_t* out, int n);
 
 /* Multi-GPU in ONE host process (no RCCL needed): the call's rows are dealt cyclically over
@@ -272,7 +283,9 @@ int rt_render_multi(const rt_scene_blob* blob, const rt_camera* cam, const rt_re
  * de-interleaves them into accum_rgb_device0 (a devices[0] buffer of opts->n_rows * W * 3
  * floats; overwritten or added to as opts->flags says). Asynchronous on hip_stream (a devices[0]
  * stream, may be NULL); stats != NULL synchronises it. Bit for bit the image of rt_render_device
- * on one device. rt_multi_info: out[0..3] = frames rendered, scene uploads, staging-buffer
+ * on one device. Consecutive frames of one handle are ordered on devices[0] (a frame waits for the
+ * previous frame's gather, whatever stream each was issued on); calls from several host threads
+ * are serialised. rt_multi_info: out[0..3] = frames rendered, scene uploads, staging-buffer
  * allocations, devices. */
 typedef struct rt_multi rt_multi;
 int rt_multi_create(const rt_scene_blob* blob, const int* devices, int n_devices, rt_multi** out);

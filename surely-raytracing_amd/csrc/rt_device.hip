@@ -24,9 +24,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -208,6 +210,23 @@ int set_err(int code, const std::string& m) {
 
 }  // namespace
 
+// The per-render state of a scene: the f64 workspace, the pool-queue word and op counters, the
+// stats events and a completion event. A render takes a slot that no render still uses (its done
+// event has fired) or one whose last render went to the same stream (stream order then protects
+// it); otherwise a new slot is made (up to kMaxSlots), so renders of one scene on different
+// streams or host threads run concurrently on their own queue words and workspaces.
+struct RenderSlot {
+  uint8_t* work = nullptr;  // row totals / segment partials / tail samples + f64 running sums
+  size_t work_bytes = 0;
+  unsigned long long* ops = nullptr;  // 32 op counters, the pool-queue word (32), profiling (40..)
+  unsigned int* queue = nullptr;
+  hipEvent_t done = nullptr;  // recorded after the render's last kernel
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // rt_stats::ms_kernel
+  hipStream_t last_stream = nullptr;
+  bool recorded = false;  // `done` has been recorded at least once
+  bool held = false;      // a render call is between acquire and release
+};
+
 struct rt_scene {
   int device = 0;
   rtl_scene_header hdr{};
@@ -218,10 +237,10 @@ struct rt_scene {
   const uint8_t *perlin = nullptr, *texels = nullptr;
   uint32_t o_mats = 0, o_texs = 0, o_lights = 0, o_loffs = 0, o_perl = 0;  // byte offsets in dev
   int sphere_light0 = -1;  // first SPHERE light record (TraceParams::sphere_light0)
-  uint8_t* work = nullptr;  // per-sample radiance slots + f64 running sums (grown on demand)
-  size_t work_bytes = 0;
-  unsigned long long* ops = nullptr;  // 32 op counters, then the pool-queue word
-  unsigned int* queue = nullptr;
+  static constexpr int kMaxSlots = 8;
+  std::vector<std::unique_ptr<RenderSlot>> slots;  // grown on demand (RenderSlot)
+  int last_slot = -1;                              // the slot of the latest render
+  std::condition_variable slot_cv;                 // a held slot was released
   int n_cu = 0;                 // compute units of the device
   size_t mem_total = (size_t)8 << 30;  // device memory (hipMemGetInfo at creation)
   size_t lds_module_max = 64u << 10;  // LDS a module (hiprtc) launch may take (device limit)
@@ -233,7 +252,6 @@ struct rt_scene {
   std::string jit_walker, jit_msg;
   int jit_state = -1;
   rtj::Kernel jit_k[4];  // [tex][staged]
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
   hipEvent_t tev[kTraceRing][2] = {};
@@ -332,7 +350,6 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   sc->hdr = F.hdr;
   hipError_t e = hipMalloc(&sc->dev, total);
   if (e == hipSuccess) e = hipMemcpy(sc->dev, host.data(), total, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&sc->ops, sizeof(unsigned long long) * 32 + 256);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&sc->n_cu, hipDeviceAttributeMultiprocessorCount,
                                                  device);
   int lds_block = 0;
@@ -344,8 +361,6 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) sc->mem_total = tot;
   }
-  if (e == hipSuccess) e = hipEventCreate(&sc->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&sc->ev1);
   for (int k = 0; k < rt_scene::kTraceRing && e == hipSuccess; ++k) {
     e = hipEventCreate(&sc->tev[k][0]);
     if (e == hipSuccess) e = hipEventCreate(&sc->tev[k][1]);
@@ -355,7 +370,6 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
     return set_err(RT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e));
   }
   sc->dev_bytes = total;
-  sc->queue = (unsigned int*)(sc->ops + 32);
   sc->nodes = (const uint32_t*)(sc->dev + o_nodes);
   sc->mats = (const uint32_t*)(sc->dev + o_mats);
   sc->texs = (const uint32_t*)(sc->dev + o_texs);
@@ -396,10 +410,13 @@ void rt_scene_destroy(rt_scene* sc) {
   (void)hipDeviceSynchronize();
   for (const rtj::Kernel& k : sc->jit_k) rtj::release_kernel(k);  // the module cache's holds
   if (sc->dev) (void)hipFree(sc->dev);
-  if (sc->work) (void)hipFree(sc->work);
-  if (sc->ops) (void)hipFree(sc->ops);
-  if (sc->ev0) (void)hipEventDestroy(sc->ev0);
-  if (sc->ev1) (void)hipEventDestroy(sc->ev1);
+  for (const auto& sl : sc->slots) {
+    if (sl->work) (void)hipFree(sl->work);
+    if (sl->ops) (void)hipFree(sl->ops);
+    if (sl->done) (void)hipEventDestroy(sl->done);
+    if (sl->ev0) (void)hipEventDestroy(sl->ev0);
+    if (sl->ev1) (void)hipEventDestroy(sl->ev1);
+  }
   for (int k = 0; k < rt_scene::kTraceRing; ++k)
     for (int j = 0; j < 2; ++j)
       if (sc->tev[k][j]) (void)hipEventDestroy(sc->tev[k][j]);
@@ -447,6 +464,77 @@ int rt_scene_jit_info(rt_scene* sc, int* state, char* msg, uint32_t msg_len) {
   return RT_OK;
 }
 
+// A slot for a render on `stream` (RenderSlot), with sc->mu held through `lock`: a free one (its
+// last render has finished, or went to the same stream), else a new one, else wait for a release.
+static int acquire_slot(rt_scene* sc, std::unique_lock<std::mutex>& lock, hipStream_t stream,
+                        RenderSlot** out) {
+  for (;;) {
+    RenderSlot* pick = nullptr;
+    for (const auto& sl : sc->slots) {
+      if (sl->held) continue;
+      if (sl->recorded && sl->last_stream == stream) {  // stream order: no wait needed
+        pick = sl.get();
+        break;
+      }
+      if (!pick) {
+        const hipError_t q = sl->recorded ? hipEventQuery(sl->done) : hipSuccess;
+        if (q == hipSuccess) pick = sl.get();
+        else if (q != hipErrorNotReady) return set_err(RT_ERR_HIP, std::string("slot event: ") + hipGetErrorString(q));
+      }
+    }
+    if (!pick && (int)sc->slots.size() < rt_scene::kMaxSlots) {
+      std::unique_ptr<RenderSlot> sl(new RenderSlot());
+      hipError_t e = hipMalloc(&sl->ops, sizeof(unsigned long long) * 64 + 256);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&sl->done, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreate(&sl->ev0);
+      if (e == hipSuccess) e = hipEventCreate(&sl->ev1);
+      if (e != hipSuccess) {
+        if (sl->ops) (void)hipFree(sl->ops);
+        if (sl->done) (void)hipEventDestroy(sl->done);
+        if (sl->ev0) (void)hipEventDestroy(sl->ev0);
+        if (sl->ev1) (void)hipEventDestroy(sl->ev1);
+        return set_err(RT_ERR_HIP, std::string("render slot: ") + hipGetErrorString(e));
+      }
+      sl->queue = (unsigned int*)(sl->ops + 32);
+      sc->slots.push_back(std::move(sl));
+      pick = sc->slots.back().get();
+    }
+    if (!pick) {  // every slot busy: wait for the oldest unheld one, or for a release
+      for (const auto& sl : sc->slots)
+        if (!sl->held) {
+          pick = sl.get();
+          break;
+        }
+      if (pick) {
+        HIP_TRY(hipEventSynchronize(pick->done));
+      } else {
+        sc->slot_cv.wait(lock);
+        continue;
+      }
+    }
+    pick->held = true;
+    sc->last_slot = (int)(std::find_if(sc->slots.begin(), sc->slots.end(),
+                                       [&](const std::unique_ptr<RenderSlot>& u) {
+                                         return u.get() == pick;
+                                       }) - sc->slots.begin());
+    *out = pick;
+    return RT_OK;
+  }
+}
+
+// Releases a held slot on every exit path of a render call.
+struct SlotHold {
+  rt_scene* sc;
+  std::unique_lock<std::mutex>& lock;
+  RenderSlot* sl = nullptr;
+  ~SlotHold() {
+    if (!sl) return;
+    if (!lock.owns_lock()) lock.lock();
+    sl->held = false;
+    sc->slot_cv.notify_all();
+  }
+};
+
 static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_render_opts* opts,
                               float* accum, void* stream_v, rt_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
@@ -473,12 +561,18 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     return set_err(RT_ERR_EMPTY_LIGHTS,
                    "empty light list with a diffuse/volume material: the reference panics "
                    "(hittable.rs:115-129)");
-  std::lock_guard<std::mutex> lock(sc->mu);
+  std::unique_lock<std::mutex> lock(sc->mu);
   hipStream_t stream = (hipStream_t)stream_v;
   HIP_TRY(hipSetDevice(sc->device));
   if (stats) std::memset(stats, 0, sizeof(*stats));
   const size_t n_px = (size_t)opts->n_rows * W;
   if (n_px == 0) return RT_OK;
+  SlotHold hold{sc, lock};
+  {
+    const int rc = acquire_slot(sc, lock, stream, &hold.sl);
+    if (rc != RT_OK) return rc;
+  }
+  RenderSlot* const sl = hold.sl;
   TraceParams P;
   std::memset(&P, 0, sizeof(P));
   P.nodes = sc->nodes;
@@ -488,8 +582,8 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   P.lights = sc->lights;
   P.light_offs = sc->light_offs;
   P.texels = sc->texels;
-  P.ops = sc->ops;
-  P.queue = sc->queue;
+  P.ops = sl->ops;
+  P.queue = sl->queue;
   P.root = sc->hdr.root;
   P.n_lights = sc->hdr.n_lights;
   P.lights_is_list = sc->hdr.lights_is_list;
@@ -754,20 +848,23 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     chunk = (chunk + 1) / 2;
   const size_t need = tot_bytes + part_bytes(chunk);
   if (!indexable(chunk)) return set_err(RT_ERR_UNSUPPORTED, "grid too large");
-  if (need > sc->work_bytes) {
-    if (sc->work) HIP_TRY(hipFree(sc->work));
-    sc->work = nullptr;
-    sc->work_bytes = 0;
-    HIP_TRY(hipMalloc(&sc->work, need));
-    sc->work_bytes = need;
+  if (need > sl->work_bytes) {
+    // the slot's previous render (another stream's, or this one's) may still read the old
+    // workspace: let it finish first
+    if (sl->recorded) HIP_TRY(hipEventSynchronize(sl->done));
+    if (sl->work) HIP_TRY(hipFree(sl->work));
+    sl->work = nullptr;
+    sl->work_bytes = 0;
+    HIP_TRY(hipMalloc(&sl->work, need));
+    sl->work_bytes = need;
   }
-  double* tot = (double*)sc->work;
-  P.part = (double*)(sc->work + tot_bytes);
-  if (ops_buf) HIP_TRY(hipMemsetAsync(sc->ops, 0, sizeof(unsigned long long) * 32, stream));
+  double* tot = (double*)sl->work;
+  P.part = (double*)(sl->work + tot_bytes);
+  if (ops_buf) HIP_TRY(hipMemsetAsync(sl->ops, 0, sizeof(unsigned long long) * 32, stream));
 #ifdef RT_PROF
-  HIP_TRY(hipMemsetAsync(sc->ops + 40, 0, sizeof(unsigned long long) * 21, stream));
+  HIP_TRY(hipMemsetAsync(sl->ops + 40, 0, sizeof(unsigned long long) * 21, stream));
 #endif
-  if (stats) HIP_TRY(hipEventRecord(sc->ev0, stream));
+  if (stats) HIP_TRY(hipEventRecord(sl->ev0, stream));
   uint64_t out_bytes = 0;
   uint32_t launches = 0;
   for (int c0 = sj0; c0 < sj0 + n_sj; c0 += chunk) {
@@ -782,7 +879,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     P.n_pools = (int)(sp.r + (sp.pairs - sp.r) * P.n_blk);
     // persistent grid: as many waves as the device holds at once (never more than pools)
     const int64_t blocks = std::min(max_blocks, ((int64_t)P.n_pools + (block / 64) - 1) / (block / 64));
-    HIP_TRY(hipMemsetAsync(sc->queue, 0, sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(sl->queue, 0, sizeof(unsigned int), stream));
     const int ring = (int)(sc->n_tev % rt_scene::kTraceRing);
     HIP_TRY(hipEventRecord(sc->tev[ring][0], stream));
     if (jfn) {
@@ -804,18 +901,22 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
     HIP_TRY(hipGetLastError());
   }
   ++sc->n_render;
-  if (stats) HIP_TRY(hipEventRecord(sc->ev1, stream));
+  if (stats) HIP_TRY(hipEventRecord(sl->ev1, stream));
+  HIP_TRY(hipEventRecord(sl->done, stream));
+  sl->recorded = true;
+  sl->last_stream = stream;
   if (stats) {
+    lock.unlock();  // the slot stays held: other renders of the scene go on meanwhile
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, sc->ev0, sc->ev1));
+    HIP_TRY(hipEventElapsedTime(&ms, sl->ev0, sl->ev1));
     stats->ms_kernel = ms;
     stats->samples = (uint64_t)n_px * (uint64_t)n_sj * (uint64_t)S;
     stats->out_bytes = out_bytes;
     stats->launches = launches;
     if (ops_buf) {
       unsigned long long h[32];
-      HIP_TRY(hipMemcpy(h, sc->ops, sizeof(h), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(h, sl->ops, sizeof(h), hipMemcpyDeviceToHost));
       for (int k = 0; k < 32; ++k) stats->ops[k] = h[k];
     }
     stats->ms_total =
@@ -867,7 +968,11 @@ int rt_scene_prof_counters(rt_scene* sc, uint64_t* out, int n) {
   HIP_TRY(hipSetDevice(sc->device));
   unsigned long long h[24] = {};
 #ifdef RT_PROF
-  HIP_TRY(hipMemcpy(h, sc->ops + 40, sizeof(h), hipMemcpyDeviceToHost));
+  if (sc->last_slot >= 0) {
+    RenderSlot* sl = sc->slots[sc->last_slot].get();
+    HIP_TRY(hipEventSynchronize(sl->done));
+    HIP_TRY(hipMemcpy(h, sl->ops + 40, sizeof(h), hipMemcpyDeviceToHost));
+  }
 #endif
   for (int k = 0; k < n && k < 24; ++k) out[k] = h[k];
   return RT_OK;
@@ -1037,6 +1142,10 @@ struct rt_multi {
   float* stage = nullptr;  // on devices[0]: every device's rows, device after device
   size_t stage_bytes = 0;
   hipEvent_t start = nullptr;  // on devices[0]: the frame's start on the caller's stream
+  // on devices[0]: the previous frame's end (its gather out of `stage`); a frame rendered on
+  // another caller stream waits for it before reusing the staging area and the device rows
+  hipEvent_t frame_done = nullptr;
+  bool frame_recorded = false;
   uint64_t frames = 0, uploads = 0, stage_allocs = 0;
   std::mutex mu;
 };
@@ -1072,6 +1181,7 @@ int rt_multi_create(const rt_scene_blob* blob, const int* devices, int n_devices
   if (rc == RT_OK) {
     hipError_t e = hipSetDevice(devices[0]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&m->start, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&m->frame_done, hipEventDisableTiming);
     if (e != hipSuccess) rc = set_err(RT_ERR_HIP, std::string("rt_multi_create: ") + hipGetErrorString(e));
   }
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -1101,6 +1211,7 @@ void rt_multi_destroy(rt_multi* m) {
   (void)hipSetDevice(m->devices[0]);
   if (m->stage) (void)hipFree(m->stage);
   if (m->start) (void)hipEventDestroy(m->start);
+  if (m->frame_done) (void)hipEventDestroy(m->frame_done);
   delete m;
   if (prev >= 0) (void)hipSetDevice(prev);
 }
@@ -1128,7 +1239,9 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
   };
   if (opts->n_rows == 0) return RT_OK;
   hipError_t e = hipSetDevice(d0);
+  if (e == hipSuccess && m->frame_recorded) e = hipStreamWaitEvent(out_stream, m->frame_done, 0);
   if (e == hipSuccess && m->stage_bytes < frame_bytes) {
+    if (m->frame_recorded) e = hipEventSynchronize(m->frame_done);
     if (m->stage) (void)hipFree(m->stage);
     m->stage = nullptr;
     m->stage_bytes = 0;
@@ -1199,6 +1312,8 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
                          out_stream, m->stage, accum_rgb_device0, (int)row_floats, opts->n_rows, G, 1);
       e = hipGetLastError();
     }
+    if (e == hipSuccess) e = hipEventRecord(m->frame_done, out_stream);
+    if (e == hipSuccess) m->frame_recorded = true;
     if (e == hipSuccess && stats) e = hipStreamSynchronize(out_stream);
     if (e != hipSuccess) rc = fail(e, "gather");
   }

@@ -26,6 +26,10 @@ def test_two_streams_render_one_scene_concurrently(gpu_available, name, kw):
     seeds = (11, 12)
     serial = [ds.render(cam, rt.make_opts(cam, seed=s))[0] for s in seeds]
     assert not np.array_equal(serial[0], serial[1])
+    ones = np.ones(serial[0].shape, np.float32)
+    # accumulate mode, serially: ones + the render's sums (rounded once, from f64)
+    serial_acc = [ds.render(cam, rt.make_opts(cam, seed=s, flags=0), accum=ones.copy())[0]
+                  for s in seeds]
     streams = [Stream(), Stream()]
     bufs = [DevBuf(serial[0].shape), DevBuf(serial[0].shape)]
     try:
@@ -40,7 +44,7 @@ def test_two_streams_render_one_scene_concurrently(gpu_available, name, kw):
             assert np.array_equal(b.download(), ref)
         # accumulate mode on both streams at once: each buffer gets its own render added
         for b in bufs:
-            b.upload(np.ones(serial[0].shape, np.float32))
+            b.upload(ones)
         for s, st, b in zip(seeds, streams, bufs):
             ds.render_device(cam, rt.make_opts(cam, seed=s, flags=0), b.ptr, st.handle)
         # a synchronous render with stats meanwhile (its own slot, third stream = NULL)
@@ -48,8 +52,8 @@ def test_two_streams_render_one_scene_concurrently(gpu_available, name, kw):
         assert np.array_equal(again, serial[0]) and stt.samples == cam.image_width * cam.image_height * cam.samples_per_pixel
         for st in streams:
             st.sync()
-        for b, ref in zip(bufs, serial):
-            assert np.array_equal(b.download(), ref + np.float32(1.0))
+        for b, ref in zip(bufs, serial_acc):
+            assert np.array_equal(b.download(), ref)
     finally:
         for b in bufs:
             b.free()
