@@ -1,16 +1,20 @@
-"""The Rust serialiser of INTEGRATION.md §1.2, transliterated arm by arm into Python over the
-reference's field names, re-serialises every preset scene and reproduces the C++ host builder's
-blob (rt_mi355x.h:47-78). There is no rustc in this image, so this is how the Rust text is
-checked: a parsed copy of the C++-built blob is turned into mirror objects (Object, Sphere, Quad,
-HittableList, BvhNode, Translate, RotateY, ConstantMedium, Material, Texture, Perlin with the
-reference's field names) and BlobWriter below (same method names and call order as the Rust)
-writes them back.
+"""The Rust crate rust/rt_mi355x (FFI mirrors + blob writer) and its reference-side arms
+rust/reference_glue/*.rs, checked without rustc (there is none in this image):
+
+* the crate's #[repr(C)] structs, extern "C" functions and constants are compared with
+  include/rt_mi355x.h field by field (names, widths, order), declaration by declaration;
+* every arm of the writer (one `// blob: <kind>` section per record kind in the glue files) is
+  reduced to its sequence of writer calls and compared with the Python transliteration below;
+* the transliteration (BlobWriter, write_blob, record, write_record, write_tables: the same
+  method names and call order as the Rust) re-serialises every preset scene from a parsed copy
+  of the C++-built blob and must reproduce it (rt_mi355x.h:47-78).
 
 Materials are values in the reference (Material is Clone), so the Rust writer deduplicates them
 by their 8-slot record; the C++ builder shares materials by pointer. Both blobs are therefore
 compared after replacing each material id by its record (textures by their records, recursively);
 the writer's own output must be a fixed point of parse + write.
 """
+import re
 import struct
 
 import numpy as np
@@ -372,3 +376,240 @@ def test_rust_serialiser_image_and_checker_textures():
     blob = sc.serialize(world)
     w = BlobWriter.serialize(*parse(blob.slots, blob.texels))
     assert w.slots == [int(v) for v in blob.slots] and bytes(w.texels) == blob.texels.tobytes()
+
+
+# ------------------------------------------------------------------ the crate's files
+from pathlib import Path  # noqa: E402
+
+REPO = Path(__file__).resolve().parent.parent
+CRATE = REPO / "rust" / "rt_mi355x"
+GLUE = REPO / "rust" / "reference_glue"
+HEADER = (REPO / "include" / "rt_mi355x.h").read_text()
+FFI = (CRATE / "src" / "ffi.rs").read_text()
+C_SIZES = {"int32_t": 4, "uint32_t": 4, "uint64_t": 8, "double": 8, "int": 4}
+R_SIZES = {"i32": 4, "u32": 4, "u64": 8, "f64": 8}
+
+
+def _strip_c_comments(t):
+    return re.sub(r"/\*.*?\*/", "", t, flags=re.S)
+
+
+def c_struct(name):
+    body = re.search(rf"typedef struct {name} \{{(.*?)\}} {name};", _strip_c_comments(HEADER), re.S)
+    assert body, name
+    fields = []
+    for decl in body.group(1).split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        m = re.match(r"(?:const\s+)?(\w+)\s*(\*?)\s*(\w+)(?:\[(\d+)\])?$", decl)
+        assert m, decl
+        ty, ptr, fname, n = m.groups()
+        fields.append((fname, 8 if ptr else C_SIZES[ty] * int(n or 1)))
+    return fields
+
+
+def rust_struct(name):
+    body = re.search(rf"pub struct {name} \{{(.*?)\n\}}", FFI, re.S)
+    assert body, name
+    fields = []
+    for line in body.group(1).splitlines():
+        line = re.sub(r"//.*", "", line).strip()
+        if not line:
+            continue
+        m = re.match(r"pub (\w+): (.+?),$", line)
+        assert m, line
+        fname, ty = m.groups()
+        if ty.startswith("*"):
+            size = 8
+        elif ty.startswith("["):
+            t, n = re.match(r"\[(\w+); (\d+)\]", ty).groups()
+            size = R_SIZES[t] * int(n)
+        else:
+            size = R_SIZES[ty]
+        fields.append((fname, size))
+    return fields
+
+
+@pytest.mark.parametrize("name", ["rt_scene_blob", "rt_camera", "rt_render_opts", "rt_stats"])
+def test_crate_structs_mirror_the_header(name):
+    assert rust_struct(name) == c_struct(name)
+
+
+def test_crate_declares_every_entry_point_of_the_header():
+    decls = {m.group(2): len([a for a in m.group(3).split(",") if a.strip() not in ("", "void")])
+             for m in re.finditer(r"^(int|void|uint64_t|const char\*)\s+(rt_\w+)\((.*?)\);",
+                                  _strip_c_comments(HEADER), re.S | re.M)}
+    assert len(decls) >= 20
+    ext = FFI[FFI.index('extern "C" {'):]
+    rust = {m.group(1): len([a for a in m.group(2).split(",") if a.strip()])
+            for m in re.finditer(r"pub fn (rt_\w+)\((.*?)\)", ext, re.S)}
+    assert rust == decls
+
+
+def test_crate_constants_match_the_header():
+    defs = dict(re.findall(r"#define (RT_\w+) \(?(-?(?:0x)?[0-9a-fA-F]+)u?\)?", HEADER))
+    enums = dict(re.findall(r"(RT_(?:OBJ|MAT|TEX)_[A-Z_]+) = (\d+)", HEADER))
+    consts = dict(re.findall(r"pub const (RT_\w+): \w+ = (-?(?:0x)?[0-9a-fA-F]+);", FFI))
+    assert len(consts) >= 30
+    for k, v in consts.items():
+        ref = defs.get(k, enums.get(k))
+        assert ref is not None, k
+        assert int(v, 0) == int(ref, 0), (k, v, ref)
+
+
+def test_crate_files_are_complete():
+    """Cargo.toml, build.rs, src/{lib,ffi,blob}.rs and one glue module per reference module;
+    every variant of the reference's Object / Transform / Material / Texture enums has its arm,
+    and no arm is elided."""
+    for f in ["Cargo.toml", "build.rs", "src/lib.rs", "src/ffi.rs", "src/blob.rs"]:
+        assert (CRATE / f).is_file(), f
+    cargo = (CRATE / "Cargo.toml").read_text()
+    assert re.search(r"^\[dependencies\]\s*$", cargo, re.M) and "links = \"rtmi355x\"" in cargo
+    glue = {p.name: p.read_text() for p in GLUE.glob("*.rs")}
+    assert set(glue) == {"object_blob.rs", "hittable_blob.rs", "transform_blob.rs",
+                         "constant_medium_blob.rs", "material_blob.rs", "texture_blob.rs",
+                         "rt_image_blob.rs", "perlin_blob.rs", "render_mi355x.rs"}
+    text = "\n".join(glue.values()) + (CRATE / "src" / "blob.rs").read_text()
+    for bad in ("todo!", "unimplemented!", "...", "/* elided"):
+        assert bad not in re.sub(r"//.*", "", text), bad
+    for enum, variants in {"Object": ["List", "Node", "Sphere", "Quad", "Transform", "Volume", "_Plane"],
+                           "Transform": ["Translate", "RotY"],
+                           "Material": ["Lambertian", "Metal", "Dielectric", "DiffuseLight", "Isotropic"],
+                           "Texture": ["Solid", "Checker", "Image", "Noise"]}.items():
+        for v in variants:
+            assert f"{enum}::{v}" in text, f"{enum}::{v}"
+
+
+def _loop_spans(body):
+    """Character ranges of the `for ... { ... }` blocks of a Rust fragment."""
+    spans = []
+    for m in re.finditer(r"\bfor\b[^{]*\{", body):
+        depth, k = 1, m.end()
+        while k < len(body) and depth:
+            depth += {"{": 1, "}": -1}.get(body[k], 0)
+            k += 1
+        spans.append((m.start(), k))
+    return spans
+
+
+def rust_arms():
+    """kind -> (the writer calls of its `// blob: kind` section, its tag literal). A call inside
+    a `for` loop is marked `*` (once in the text, any number of times at run time)."""
+    arms = {}
+    for p in GLUE.glob("*.rs"):
+        parts = re.split(r"//\s*blob:\s*(\w+)[^\n]*\n", p.read_text())
+        for kind, body in zip(parts[1::2], parts[2::2]):
+            body = re.split(r"\n\s*\}\s*\n\s*(?:\w+::\w+|impl|fn)", body)[0]
+            loops = _loop_spans(body)
+            seq = []
+            for c in re.finditer(r"w\.(i|f|v3|bbox|material|texture|perlin)\(|(\.write_blob)\(", body):
+                name = "child" if c.group(2) else c.group(1)
+                seq.append(name + ("*" if any(a <= c.start() < b for a, b in loops) else ""))
+            tag = re.search(r"w\.i\((\d+)\)|r\[0\] = (\d+);", body)
+            arms[kind] = (seq, int(tag.group(1) or tag.group(2)) if tag else None)
+    return arms
+
+
+def _matches(rust_seq, calls):
+    """The run-time calls are the Rust sequence with each `X*` repeated one or more times."""
+    pat = "".join(f"(?:{t[:-1]},)+" if t.endswith("*") else f"{t}," for t in rust_seq)
+    return re.fullmatch(pat, "".join(c + "," for c in calls)) is not None
+
+
+class _Trace(BlobWriter):
+    """The transliteration's writer, recording its calls (children not descended into)."""
+
+    def __init__(self):
+        super().__init__()
+        self.calls = []
+
+    def f(self, x):
+        self.calls.append("f")
+        super().f(x)
+
+    def i(self, x):
+        self.calls.append(("i", int(x)))
+        super().i(x)
+
+    def v3(self, v):
+        self.calls.append("v3")
+        for x in v:
+            BlobWriter.f(self, x)
+
+    def bbox(self, b):
+        self.calls.append("bbox")
+        for x in b:
+            BlobWriter.f(self, x)
+
+    def material(self, m):
+        self.calls.append("material")
+        return 0
+
+    def texture(self, t):
+        self.calls.append("texture")
+        return 0
+
+    def perlin(self, p):
+        self.calls.append("perlin")
+        return 0
+
+
+def _trace(fn, obj, **ids):
+    w = _Trace()
+    w.tex_ids.update(ids.get("tex_ids", {}))
+    w.perlin_ids.update(ids.get("perlin_ids", {}))
+    global write_blob
+    real = write_blob
+
+    def shallow(o, ww):
+        if ww is w and o is not obj:
+            w.calls.append("child")
+        else:
+            real(o, ww)
+    write_blob = shallow
+    try:
+        fn(obj, w)
+    finally:
+        write_blob = real
+    tag = next(c[1] for c in w.calls if isinstance(c, tuple))
+    return [c[0] if isinstance(c, tuple) else c for c in w.calls], tag
+
+
+def test_rust_arms_match_the_transliteration():
+    arms = rust_arms()
+    leaf = Obj("sphere", mat=Mat("lambertian", texture=Tex("solid", color_value=(1, 1, 1))),
+               center=(0, 0, 0), radius=1.0, center_vec=None, bbox=(0,) * 6)
+    solid = Tex("solid", color_value=(1, 2, 3))
+    noise = Tex("noise", scale=4.0, noise=Tex("perlin", ranvec=[(1, 0, 0)] * 256,
+                                              perm_x=list(range(256)), perm_y=list(range(256)),
+                                              perm_z=list(range(256))))
+    cases = {
+        "sphere": (write_blob, leaf),
+        "quad": (write_blob, Obj("quad", mat=leaf.mat, q=(0, 0, 0), u=(1, 0, 0), v=(0, 1, 0),
+                                 normal=(0, 0, 1), w=(0, 0, 1), d=0.0, area=1.0, bbox=(0,) * 6)),
+        "list": (write_blob, Obj("list", objects=[leaf], bbox=(0,) * 6)),
+        "node": (write_blob, Obj("node", left=leaf, right=leaf, bbox=(0,) * 6)),
+        "translate": (write_blob, Obj("translate", offset=(1, 2, 3), bbox=(0,) * 6, object=leaf)),
+        "rot_y": (write_blob, Obj("rot_y", sin_theta=0.5, cos_theta=0.8, bbox=(0,) * 6, object=leaf)),
+        "volume": (write_blob, Obj("volume", phase_function=Mat("isotropic", albedo=solid),
+                                   neg_inv_density=-2.0, boundary_bbox=(0,) * 6, boundary=leaf)),
+        "solid": (write_record, solid),
+        "checker": (write_record, Tex("checker", inv_scale=2.0, even=solid, odd=solid)),
+        "image": (write_record, Tex("image", image_width=2, image_height=1, image=bytes(6))),
+        "noise": (write_record, noise),
+        "perlin": (write_tables, noise.noise),
+    }
+    ids = {"tex_ids": {id(solid): 0}, "perlin_ids": {id(noise.noise): 0}}
+    for kind, (fn, obj) in cases.items():
+        assert kind in arms, f"no `// blob: {kind}` arm in rust/reference_glue"
+        seq, tag = _trace(fn, obj, **ids) if kind != "perlin" else (["v3"] * 256 + ["i"] * 768, 0)
+        rseq, rtag = arms[kind]
+        assert _matches(rseq, seq), (kind, rseq, seq)
+        if kind != "perlin":
+            assert rtag == tag, (kind, rtag, tag)
+    mats = {"lambertian": 1, "metal": 2, "dielectric": 3, "diffuse_light": 4, "isotropic": 5}
+    for kind, code in mats.items():
+        rseq, rtag = arms[kind]
+        assert rtag == code, kind
+        assert rseq == (["texture"] if code in (1, 4, 5) else []), (kind, rseq)
