@@ -50,6 +50,13 @@ CONFIGS = {
 }
 
 
+# The one-GPU share probe of the C2 frame (tools_gpu/scaling_probe.py, round 3): full-frame
+# kernel time / (N x slowest share's kernel time). A projection, reported beside a measured N > 1
+# line, never in place of one.
+SCALING_PROJECTION = {("BASELINE configs[1]", 2): 0.983, ("BASELINE configs[1]", 4): 0.974,
+                      ("BASELINE configs[1]", 8): 0.939}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,7 +145,7 @@ def main():
 
     import surely_rt as rt
     from surely_rt import roofline
-    from surely_rt.parallel import cyclic_rows, gather_frame, max_rows
+    from surely_rt.parallel import cyclic_rows, gather_frame, max_rows, rank_report
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -174,7 +181,10 @@ def main():
         ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        return gather_frame(local_buf.cpu() if rehearse else local_buf, H, rank, world)
+        out = gather_frame(local_buf.cpu() if rehearse else local_buf, H, rank, world)
+        if ev is not None:
+            ev[2].record(stream)  # the gather has completed on this stream
+        return out
 
     # ---- op counts for the roofline (outside the timed region; deterministic)
     ops = None
@@ -193,7 +203,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
               for _ in range(args.steps)]
     t0 = time.perf_counter()
     frame = None
@@ -203,11 +213,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    local_elapsed = elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    step_gpu_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(1, args.steps)
+    step_gpu_ms = sum(e[0].elapsed_time(e[1]) for e in events) / max(1, args.steps)
+    gather_ms = sum(e[1].elapsed_time(e[2]) for e in events) / max(1, args.steps)
     # the roofline's kernel: rt_trace alone (HIP events the library records around its launches
     # on this stream), excluding the per-pixel reduction that step_gpu_ms also contains
     trace = ds.trace_ms(args.steps)
@@ -215,6 +227,12 @@ def main():
 
     # the product kernel that ran: scene-specialised (world walker generated from the scene,
     # compiled by hiprtc at the first render, outside the timed region) or the interpreter
+    # N > 1: every rank's kernel, render and gather times to rank 0 (outside the timed region)
+    ranks = None
+    if world > 1:
+        ranks = rank_report({"trace_ms": kernel_ms, "render_ms": step_gpu_ms,
+                             "gather_ms": gather_ms, "step_ms": local_elapsed / args.steps * 1e3,
+                             "rows": n}, rank, world)
     jstate, jmsg = ds.jit_info()
     walker = ("scene-specialised (rt_jit.cpp, hiprtc)" if jstate == 1
               else f"interpreter ({jmsg.splitlines()[0] if jmsg else 'jit state %d' % jstate})")
@@ -242,6 +260,17 @@ def main():
                 "walker": walker,
             },
         }
+        if ranks is not None:
+            res["ranks"] = ranks
+            res["ranks"]["note"] = ("per rank: rt_trace ms (HIP events), render ms (rt_trace + "
+                                    "rt_reduce), gather ms (the frame gather to rank 0, events "
+                                    "on the rank's stream), step ms (host clock), rows")
+            proj = SCALING_PROJECTION.get((args.config_name, world))
+            if proj is not None:
+                res["scaling_projection"] = {
+                    "efficiency": proj, "source": "profiles/r03_scaling_probe_adaptive.log",
+                    "kind": "projection, not a measurement: one GPU renders each rank's cyclic "
+                            "share in turn; efficiency = full frame / (N x slowest share)"}
         if ops is not None:
             # flops of the rank-0 launch (its share of rows) over its kernel time; kernel_ms is
             # per render, i.e. summed over the render's launches (stratum-row chunks)

@@ -758,9 +758,10 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
         const int regs = (jk.regs + 7) & ~7;
         char why[256];
         std::snprintf(why, sizeof(why),
-                      "scene-specialised kernel: %d regs, max %d threads, %d B static LDS, "
+                      "scene-specialised kernel%s: %d regs, max %d threads, %d B static LDS, "
                       "%d B scratch/lane; launch %d threads, %zu B dynamic LDS",
-                      jk.regs, jk.max_threads, jk.static_lds, jk.scratch, block, lds_bytes);
+                      jk.cached ? " (code-object cache)" : "", jk.regs, jk.max_threads,
+                      jk.static_lds, jk.scratch, block, lds_bytes);
         if (jk.max_threads < block || regs * waves_per_simd > 512 ||
             (size_t)jk.static_lds + lds_bytes > sc->lds_module_max ||
             (size_t)jk.static_lds > static_lds) {

@@ -21,7 +21,9 @@
 // (source, device) for the process.
 #include "rt_jit.hpp"
 
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <unistd.h>
 
 #include <cmath>
 #include <cstdio>
@@ -29,6 +31,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <fstream>
+#include <iterator>
 #include <sstream>
 #include <utility>
 #include <vector>
@@ -37,6 +41,52 @@
 
 namespace rtj {
 namespace {
+// FNV-1a, 64 bits, over a sequence of strings (each terminated by its length)
+uint64_t fnv1a(uint64_t h, const char* p, size_t n) {
+  for (size_t i = 0; i < n; ++i) h = (h ^ (uint8_t)p[i]) * 0x100000001b3ull;
+  for (int k = 0; k < 8; ++k) h = (h ^ (uint8_t)(n >> (8 * k))) * 0x100000001b3ull;
+  return h;
+}
+
+// Where the code object of this translation unit lives in the code-object cache, or "" when the
+// cache is off. The directory is RT_JIT_CACHE_DIR, by default jit_cache/ next to this library
+// (build/jit_cache, filled at build time by tools/jit_cache_fill.py for the benchmark scenes); the
+// file name is a 128-bit hash of the source, every header text and every compile option (which
+// include the target), so an edited header or option never loads a stale object. RT_JIT_CACHE=0
+// turns the cache off. Why: the hiprtc a process binds to is whichever libhiprtc.so.7 it loaded
+// first (PyTorch's bundled ROCm 7.0 compiler once torch is imported, the system's 7.2 one
+// otherwise or under rocprofv3, which preloads the system runtime), and the two allocate
+// registers differently (final_scene: 163 VGPRs and no spills against 168 + 71 spilled); with the
+// cache the benchmark, the tests and the profiler all run the one binary built at build time.
+std::string cache_path(const std::string& src, const std::vector<const char*>& headers,
+                       const std::vector<const char*>& opts) {
+  const char* off = std::getenv("RT_JIT_CACHE");
+  if (off && std::strcmp(off, "0") == 0) return "";
+  std::string dir;
+  if (const char* d = std::getenv("RT_JIT_CACHE_DIR")) {
+    dir = d;
+  } else {
+    Dl_info info;
+    if (!dladdr((const void*)&fnv1a, &info) || !info.dli_fname) return "";
+    dir = info.dli_fname;
+    const size_t slash = dir.rfind('/');
+    dir = (slash == std::string::npos ? std::string(".") : dir.substr(0, slash)) + "/jit_cache";
+  }
+  uint64_t a = 0xcbf29ce484222325ull, b = 0x84222325cbf29ce4ull;
+  auto add = [&](const char* p) {
+    const size_t n = std::strlen(p);
+    a = fnv1a(a, p, n);
+    b = fnv1a(b ^ 0x9e3779b97f4a7c15ull, p, n);
+  };
+  add(src.c_str());
+  for (const char* h : headers) add(h);
+  for (const char* o : opts) add(o);
+  char name[64];
+  std::snprintf(name, sizeof name, "/%016llx%016llx.co", (unsigned long long)a,
+                (unsigned long long)b);
+  return dir + name;
+}
+
 
 // Largest scene the generator unrolls (primitive tests per world query) and the packed winner
 // code's range: (record + 1) | frame_id << 24, frame_id = the frame's ordinal in the walk (0 = the
@@ -553,20 +603,32 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
       "typedef unsigned int uint32_t; typedef unsigned long uint64_t; typedef signed char int8_t;\n"
       "typedef short int16_t; typedef int int32_t; typedef long int64_t;\n";
   std::vector<const char*> hs, hn;
+  // diagnostics (register-allocation work without rebuilding the library): RT_JIT_SRC_DIR, a
+  // ':'-separated list of directories, replaces the embedded headers by the files found there
+  static thread_local std::vector<std::string> override_text;
+  override_text.assign(kJitSrcCount, std::string());
+  const char* src_dirs = std::getenv("RT_JIT_SRC_DIR");
   for (int k = 0; k < kJitSrcCount; ++k) {
-    hs.push_back(kJitSrcText[k]);
+    const char* text = kJitSrcText[k];
+    if (src_dirs && *src_dirs) {
+      std::istringstream dirs(src_dirs);
+      for (std::string d; std::getline(dirs, d, ':');) {
+        std::ifstream f(d + "/" + kJitSrcNames[k], std::ios::binary);
+        if (!f) continue;
+        std::ostringstream buf;
+        buf << f.rdbuf();
+        override_text[k] = buf.str();
+        text = override_text[k].c_str();
+        break;
+      }
+    }
+    hs.push_back(text);
     hn.push_back(kJitSrcNames[k]);
   }
   hs.push_back(kStdint);
   hn.push_back("stdint.h");
   hs.push_back("#pragma once\n");
   hn.push_back("hip/hip_runtime.h");
-  hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_trace_jit.hip", (int)hs.size(), hs.data(),
-                          hn.data()) != HIPRTC_SUCCESS) {
-    *log = "hiprtcCreateProgram failed";
-    return RT_ERR_HIP;
-  }
   const std::string off = "--offload-arch=" + arch;
   // the ahead-of-time build's arithmetic flags (Makefile HIPFLAGS): contraction off, so every
   // fma is the one written in rt_kernel.h and the generated walker computes the same bits
@@ -658,6 +720,25 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
     for (std::string w; in >> w;) extra.push_back(w);
   }
   for (const std::string& w : extra) opts.push_back(w.c_str());
+  // The code-object cache (cache_path): a translation unit compiled before with the same
+  // headers, options and target is loaded instead of compiled again.
+  const std::string cached = cache_path(src, hs, opts);
+  if (!cached.empty()) {
+    std::ifstream f(cached, std::ios::binary);
+    if (f) {
+      code->assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+      if (!code->empty()) {
+        *log = "code-object cache: " + cached;
+        return 0;
+      }
+    }
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_trace_jit.hip", (int)hs.size(), hs.data(),
+                          hn.data()) != HIPRTC_SUCCESS) {
+    *log = "hiprtcCreateProgram failed";
+    return RT_ERR_HIP;
+  }
   const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t n = 0;
   hiprtcGetProgramLogSize(prog, &n);
@@ -673,6 +754,16 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   code->resize(code_size);
   hiprtcGetCode(prog, code->data());
   hiprtcDestroyProgram(&prog);
+  const char* wr = std::getenv("RT_JIT_CACHE_WRITE");
+  if (!cached.empty() && wr && std::strcmp(wr, "1") == 0) {  // populate the cache (tools/jit_cache_fill.py)
+    const std::string tmp = cached + ".tmp" + std::to_string((unsigned long)getpid());
+    if (FILE* f = std::fopen(tmp.c_str(), "wb")) {
+      const bool ok = std::fwrite(code->data(), 1, code->size(), f) == code->size();
+      std::fclose(f);
+      if (ok) std::rename(tmp.c_str(), cached.c_str());
+      else std::remove(tmp.c_str());
+    }
+  }
   if (const char* dump = std::getenv("RT_JIT_DUMP")) {  // diagnostics: the code object as built
     if (FILE* f = std::fopen(dump, "wb")) {
       std::fwrite(code->data(), 1, code->size(), f);
@@ -729,7 +820,9 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
                std::string* log) {
   const std::string s = kernel_source(walker, f);
   std::lock_guard<std::mutex> lock(g_mu);
-  auto key = std::make_pair(device, s);
+  // compile() reads RT_JIT_SRC_DIR's headers when set (diagnostics): part of the module's identity
+  const char* src_dirs = std::getenv("RT_JIT_SRC_DIR");
+  auto key = std::make_pair(device, src_dirs ? s + "//" + src_dirs : s);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
     ++it->second.holds;
@@ -749,6 +842,7 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
   const int rc = compile(s, arch, &code, log);
   if (rc != 0) return rc;
   Kernel k;
+  k.cached = log->rfind("code-object cache", 0) == 0;
   if (hipModuleLoadData(&k.mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&k.fn, k.mod, "rt_trace_jit") != hipSuccess) {
     *log = "hipModuleLoadData / hipModuleGetFunction failed";

@@ -33,6 +33,7 @@ struct Kernel {
   // code-object resources as the runtime reports them (hipFuncGetAttribute), checked against
   // the launch before every first use (rt_device.hip)
   int regs = 0, max_threads = 0, static_lds = 0, scratch = 0;
+  bool cached = false;  // loaded from the code-object cache (rt_jit.cpp cache_path), not compiled
 };
 int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* out,
                std::string* log);

@@ -2151,7 +2151,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   __shared__ double sh_row[ROWS ? 3 * NB : 1];
   const int tid = threadIdx.x;
 
-  d3 ro = mk(0., 0., 0.), rd = ro, beta = ro, Lp = ro;
+  d3 ro = mk(0., 0., 0.), rd = ro, beta = ro;
   double tm = 0.;
   // remaining bounces (low 24 bits, render.rs:260) | special-value state RT_XS_* << 24
   int depth = 0;
@@ -2318,7 +2318,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       rd = ps - origin;
       tm = rnd(g);
       beta = mk(1., 1., 1.);
-      Lp = mk(0., 0., 0.);
       depth = Q->max_depth;  // RT_XS_* cleared
       alive = true;
       fresh = false;
@@ -2340,7 +2339,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // lanes then share ONE end_sample. ray_color's depth guard (render.rs:260-262) is applied
     // where the depth is decremented (a fresh path starts with max_depth >= 1; at max_depth 0
     // the camera-ray block ends every sample at once).
-    bool term = false;
+    // A path gathers radiance only where it ends (a miss adds beta * background, a light hit beta *
+    // emission, render.rs:272, 292-309; every other bounce adds the zero emission of a non-light,
+    // and a zero-pdf bounce restarts the sum at 0), so its radiance is 0 until that bounce and
+    // then 0 + beta * X = beta * X exactly: no running radiance is carried across bounces.
+    bool term = false, emit_end = false;
+    d3 Le;                      // the ending lanes' radiance (undefined on the others)
     d3 p_next, d_next, f_next;  // the scattered ray and this bounce's throughput factor
     const bool run = COUNT ? alive : true;
     if (!run) {
@@ -2373,8 +2377,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 #endif
     if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
-      Lp = Lp + beta * karr3(kparams()->bg);
-      term = true;
+      Le = beta * karr3(kparams()->bg);
+      term = emit_end = true;
       break;
     }
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
@@ -2432,8 +2436,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     PROF(3);
     if ((SC & kScLight) && kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
-      if (front) Lp = vfma(1.0, beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C), Lp);
-      term = true;
+      Le = front ? beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C) : mk(0., 0., 0.);
+      term = emit_end = true;
       break;
     }
     if ((SC & kScMetal) && kind == RT_MAT_METAL) {  // material.rs:124-134
@@ -2584,7 +2588,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 #ifndef RT_ABL_NOXS  // ablation build: no special-value tracking (cost of RT_XS_*)
       if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
         depth |= (int)((RT_XS_ON | xs_nan_bits(atten * s_pdf, beta)) << 24);
-        Lp = mk(0., 0., 0.);
         beta = mk(1., 1., 1.);
         factor = beta;
       }
@@ -2604,12 +2607,17 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       ro = p_next;
       rd = d_next;
       beta = beta * f_next;
+      // the product is formed here: left to itself the compiler sinks it to beta's next use (the
+      // following bounce, past the pool scheduling and the camera-ray block), which keeps the
+      // three factors live across the loop's back edge and spills them (ROCm 7.2: scratch
+      // stores and three serialised reloads per bounce at C3 and C4)
+      asm volatile("" : "+v"(beta.x), "+v"(beta.y), "+v"(beta.z));
       --depth;  // ending lanes had depth >= 1: the RT_XS_* bits above it are untouched
       const bool cut = !term && (depth & 0xffffff) == 0;
       C.inc_if(RT_OP_DEPTH_CUTOFF, cut);
       term |= cut;
     }
-    if (term & alive) end_sample(Lp);
+    if (term & alive) end_sample(emit_end ? Le : mk(0., 0., 0.));
   }
 #ifdef RT_PROF
   PROF(7);

@@ -58,3 +58,24 @@ def gather_frame(local, height: int, rank: int, world: int, dst: int = 0):
     if rank != dst:
         return None
     return deinterleave(torch.stack(bufs), height, world)
+
+
+def rank_report(local: dict, rank: int, world: int, dst: int = 0):
+    """Every rank's timings (a dict of floats: rt_trace ms, render ms, gather ms, ...) gathered
+    to `dst` (torch.distributed.gather_object; outside any timed region). On dst: each key as a
+    per-rank list, plus the slowest / fastest rank ratio of the render and kernel times (the
+    share imbalance a strong-scaling step pays). None elsewhere."""
+    import torch.distributed as dist
+
+    objs = [None] * world if rank == dst else None
+    dist.gather_object(local, objs, dst=dst)
+    if rank != dst:
+        return None
+    rep = {f"{k}_per_rank": [round(float(o[k]), 3) for o in objs] for k in sorted(local)}
+    for k in ("trace_ms", "render_ms", "gather_ms"):
+        if k in local:
+            v = [float(o[k]) for o in objs]
+            rep[f"{k}_slowest"] = round(max(v), 3)
+            if k != "gather_ms" and min(v) > 0:
+                rep[f"{k}_slowest_fastest_ratio"] = round(max(v) / min(v), 4)
+    return rep

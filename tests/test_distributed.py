@@ -83,3 +83,61 @@ def test_cyclic_rows_partition():
     out = deinterleave(g, 5, 2)
     assert np.array_equal(out[0], g[0, 0]) and np.array_equal(out[1], g[1, 0])
     assert np.array_equal(out[4], g[0, 2])
+
+
+def _report_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "surely-raytracing_amd"))
+    from surely_rt.parallel import rank_report
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = rank_report({"trace_ms": 10.0 + rank, "render_ms": 11.0 + 2 * rank,
+                           "gather_ms": 0.5 * (rank + 1), "step_ms": 12.0, "rows": 400 - rank},
+                          rank, world)
+        if rank == 0:
+            q.put(rep)
+        else:
+            q.put(rep is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_report_fields_for_the_n_gpu_bench_line():
+    """bench.py --gpus N > 1 puts every rank's rt_trace / render / gather ms and the slowest /
+    fastest rank ratio into the rank-0 JSON line (surely_rt.parallel.rank_report), gathered
+    over the process group (gloo here, RCCL on the GPU node)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rep = next(g for g in got if isinstance(g, dict))
+    assert True in got
+    assert rep["trace_ms_per_rank"] == [10.0, 11.0]
+    assert rep["render_ms_per_rank"] == [11.0, 13.0]
+    assert rep["gather_ms_per_rank"] == [0.5, 1.0] and rep["gather_ms_slowest"] == 1.0
+    assert rep["rows_per_rank"] == [400.0, 399.0]
+    assert rep["render_ms_slowest_fastest_ratio"] == round(13.0 / 11.0, 4)
+    assert rep["trace_ms_slowest_fastest_ratio"] == round(11.0 / 10.0, 4)
+
+
+def test_bench_reports_ranks_and_projection_for_n_gpus():
+    """The rank-0 JSON assembly of bench.py names the per-rank fields and labels the one-GPU
+    share probe as a projection (source text check: the N > 1 path needs GPUs to run)."""
+    from pathlib import Path
+
+    src = (Path(__file__).resolve().parent.parent / "bench.py").read_text()
+    assert 'res["ranks"] = ranks' in src and "rank_report(" in src
+    assert '"scaling_projection"' in src and "projection, not a measurement" in src
+    assert "gather_ms" in src and "ev[2].record(stream)" in src
