@@ -2,6 +2,7 @@
 #   build/librtmi355x.so   HIP kernels + C ABI (include/rt_mi355x.h)   <- the product
 #   build/librthost.so     C++ scene builder + output stage (include/rt_host.h)
 #   build/rt_render_cli    main.rs-equivalent host program (preset -> PPM)
+#   build/librtgather.so   RCCL framebuffer gather for one process per GPU (include/rt_gather.h)
 #   oracle/_build/*.so     CPU restatement (test infrastructure only)
 PKG      := surely-raytracing_amd
 CSRC     := $(PKG)/csrc
@@ -18,12 +19,13 @@ DEV_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_flatten.cpp $(CSRC)/rt_obvh.cpp $(C
 DEV_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_rng.h $(CSRC)/rt_layout.h $(CSRC)/rt_flatten.hpp $(CSRC)/rt_jit.hpp include/rt_mi355x.h $(BUILD)/rt_jit_sources.inc
 JIT_HDR  := $(CSRC)/rt_kernel.h $(CSRC)/rt_layout.h include/rt_mi355x.h $(CSRC)/rt_rng.h
 
-.PHONY: all device host oracle cli clean
-all: device host oracle cli
+.PHONY: all device host oracle cli gather clean
+all: device host oracle cli gather
 
 device: $(BUILD)/librtmi355x.so
 host: $(BUILD)/librthost.so
 cli: $(BUILD)/rt_render_cli
+gather: $(BUILD)/librtgather.so
 oracle: oracle/_build/liboracle_f32.so oracle/_build/liboracle_f64.so oracle/_build/liboracle_f64fma.so
 
 # device headers embedded for the scene-specialised kernels compiled at run time (rt_jit.cpp)
@@ -34,6 +36,10 @@ $(BUILD)/rt_jit_sources.inc: $(JIT_HDR) $(CSRC)/embed_sources.py
 $(BUILD)/librtmi355x.so: $(DEV_SRC) $(DEV_HDR)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -shared $(DEV_SRC) -o $@ -lhiprtc
+
+$(BUILD)/librtgather.so: $(CSRC)/rt_gather.hip include/rt_gather.h include/rt_mi355x.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -shared $(CSRC)/rt_gather.hip -o $@ -lrccl
 
 $(BUILD)/librthost.so: $(HOST_SRC) $(CSRC)/host/scene.hpp include/rt_host.h include/rt_mi355x.h
 	@mkdir -p $(BUILD)

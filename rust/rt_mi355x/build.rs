@@ -1,4 +1,5 @@
-// Link against librtmi355x.so (make device -> build/librtmi355x.so of this repository).
+// Link against librtmi355x.so (make device -> build/librtmi355x.so of this repository) and, with
+// the "rccl-gather" feature, librtgather.so (make gather).
 // RT_MI355X_LIB_DIR overrides the default ../../build (relative to this crate); running the
 // binary needs that directory and /opt/rocm/lib on LD_LIBRARY_PATH.
 use std::env;
@@ -13,4 +14,7 @@ fn main() {
     println!("cargo:rustc-link-search=native={}", dir.display());
     println!("cargo:rustc-link-search=native=/opt/rocm/lib");
     println!("cargo:rustc-link-lib=dylib=rtmi355x");
+    if env::var_os("CARGO_FEATURE_RCCL_GATHER").is_some() {
+        println!("cargo:rustc-link-lib=dylib=rtgather"); // and librccl.so through it
+    }
 }

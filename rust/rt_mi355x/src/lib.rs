@@ -5,11 +5,15 @@
 //! * [`blob`]: the scene-blob writer; the reference's types implement its traits in
 //!   rust/reference_glue/ (child modules of their own modules).
 //! * [`Scene`], [`render_blob`]: safe wrappers (status codes -> `Result`, `rt_last_error`).
+//! * `gather` (feature "rccl-gather"): librtgather.so, the RCCL frame gather of one process per
+//!   GPU (include/rt_gather.h).
 //!
 //! No dependencies; link with build.rs (RT_MI355X_LIB_DIR).
 
 pub mod blob;
 pub mod ffi;
+#[cfg(feature = "rccl-gather")]
+pub mod gather;
 
 pub use blob::{Blob, BlobWriter, MaterialRecord, PerlinTables, TextureRecord, WriteBlob};
 

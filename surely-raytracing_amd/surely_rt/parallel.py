@@ -79,3 +79,77 @@ def rank_report(local: dict, rank: int, world: int, dst: int = 0):
             if k != "gather_ms" and min(v) > 0:
                 rep[f"{k}_slowest_fastest_ratio"] = round(max(v) / min(v), 4)
     return rep
+
+
+# ---------------------------------------------------------------- the C-ABI RCCL gather
+_gather = None
+
+
+def gather_lib():
+    """librtgather.so (include/rt_gather.h): the framebuffer gather over RCCL for a host that runs
+    one process per GPU without torch.distributed. Raises if it is not built."""
+    global _gather
+    if _gather is None:
+        import ctypes as C
+        from pathlib import Path
+
+        path = Path(__file__).resolve().parent.parent.parent / "build" / "librtgather.so"
+        if not path.exists():
+            raise RuntimeError(f"{path} missing: run `make gather`")
+        lib = C.CDLL(str(path))
+        p = C.c_void_p
+        sig = {
+            "rt_gather_last_error": (C.c_char_p, []),
+            "rt_gather_unique_id": (C.c_int, [C.c_char_p]),
+            "rt_gather_comm_create": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int,
+                                                C.POINTER(p)]),
+            "rt_gather_comm_destroy": (None, [p]),
+            "rt_gather_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+            "rt_gather_max_rows": (C.c_int, [C.c_int, C.c_int]),
+            "rt_gather_frame": (C.c_int, [p, p, C.c_int, C.c_int, p, p, p]),
+            "rt_gather_deinterleave": (C.c_int, [p, C.c_int, C.c_int, C.c_int, p, p]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        _gather = lib
+    return _gather
+
+
+class RcclFrameGather:
+    """One rank's member of an RCCL communicator for the frame gather (rt_gather_comm)."""
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
+        import ctypes as C
+
+        self._lib = gather_lib()
+        h = C.c_void_p()
+        rc = self._lib.rt_gather_comm_create(uid, world, rank, device, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(self._lib.rt_gather_last_error().decode())
+        self._h, self.world, self.rank = h, world, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        buf = C.create_string_buffer(128)
+        lib = gather_lib()
+        if lib.rt_gather_unique_id(buf) != 0:
+            raise RuntimeError(lib.rt_gather_last_error().decode())
+        return buf.raw
+
+    def gather(self, local_ptr: int, width: int, height: int, scratch_ptr: int, frame_ptr: int,
+               stream: int = 0):
+        import ctypes as C
+
+        rc = self._lib.rt_gather_frame(self._h, C.c_void_p(local_ptr), width, height,
+                                       C.c_void_p(scratch_ptr or None),
+                                       C.c_void_p(frame_ptr or None), C.c_void_p(stream or None))
+        if rc != 0:
+            raise RuntimeError(self._lib.rt_gather_last_error().decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rt_gather_comm_destroy(self._h)
+            self._h = None

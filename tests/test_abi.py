@@ -19,10 +19,11 @@ def _declared(header: str):
 
 
 @pytest.mark.parametrize("header,lib", [("rt_mi355x.h", "librtmi355x.so"),
-                                        ("rt_host.h", "librthost.so")])
+                                        ("rt_host.h", "librthost.so"),
+                                        ("rt_gather.h", "librtgather.so")])
 def test_exports_every_declared_symbol(header, lib):
     names = _declared(header)
-    assert len(names) >= 8
+    assert len(names) >= 7
     so = C.CDLL(str(REPO / "build" / lib))
     missing = [n for n in names if not hasattr(so, n)]
     assert not missing, missing
@@ -93,3 +94,18 @@ def test_product_path_fails_loudly_without_library(tmp_path):
     """No CPU fallback: with the HIP library absent, loading the render path raises."""
     with pytest.raises(RuntimeError, match="HIP library is required"):
         rt.load_device_lib(tmp_path / "librtmi355x.so")
+
+
+def test_gather_row_layout_host_functions():
+    """rt_gather_rows / rt_gather_max_rows (host-only): the cyclic tiling of bench.py and
+    surely_rt.parallel (rank r renders rows r, r + N, ...), padded to ceil(H / N)."""
+    from surely_rt.parallel import cyclic_rows, gather_lib, max_rows
+
+    g = gather_lib()
+    for H in (1, 7, 800, 2160):
+        for N in (1, 2, 3, 8):
+            assert g.rt_gather_max_rows(H, N) == max_rows(H, N)
+            assert sum(g.rt_gather_rows(H, N, r) for r in range(N)) == H
+            for r in range(N):
+                assert g.rt_gather_rows(H, N, r) == cyclic_rows(H, r, N)[2]
+    assert g.rt_gather_rows(5, 0, 0) == 0 and g.rt_gather_max_rows(0, 4) == 0

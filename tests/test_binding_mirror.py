@@ -613,3 +613,24 @@ def test_rust_arms_match_the_transliteration():
         rseq, rtag = arms[kind]
         assert rtag == code, kind
         assert rseq == (["texture"] if code in (1, 4, 5) else []), (kind, rseq)
+
+
+def test_crate_gather_module_mirrors_rt_gather_h():
+    """src/gather.rs declares every entry point of include/rt_gather.h with its arity, behind the
+    "rccl-gather" feature that build.rs turns into -lrtgather."""
+    header = _strip_c_comments((REPO / "include" / "rt_gather.h").read_text())
+    decls = {m.group(2): len([a for a in m.group(3).split(",") if a.strip() not in ("", "void")])
+             for m in re.finditer(r"^(int|void|const char\*)\s+(rt_gather_\w+)\((.*?)\);",
+                                  header, re.S | re.M)}
+    assert len(decls) == 8
+    src = (CRATE / "src" / "gather.rs").read_text()
+    ext = src[src.index('extern "C" {'):src.index("\n}\n", src.index('extern "C" {'))]
+    rust = {m.group(1): len([a for a in m.group(2).split(",") if a.strip()])
+            for m in re.finditer(r"pub fn (rt_gather_\w+)\((.*?)\)", ext, re.S)}
+    assert rust == decls
+    idb = re.search(r"#define RT_GATHER_ID_BYTES (\d+)", header).group(1)
+    assert f"pub const RT_GATHER_ID_BYTES: usize = {idb};" in src
+    assert '#[link(name = "rtgather")]' in src
+    assert 'rccl-gather = []' in (CRATE / "Cargo.toml").read_text()
+    assert "CARGO_FEATURE_RCCL_GATHER" in (CRATE / "build.rs").read_text()
+    assert '#[cfg(feature = "rccl-gather")]\npub mod gather;' in (CRATE / "src" / "lib.rs").read_text()
