@@ -602,10 +602,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   const bool tex = sc->hdr.has_textures != 0;
   const bool bvh = sc->hdr.has_bvh != 0;
   const int block = bvh ? kBlockBvh : kBlock;
-  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc, and the row
-  // totals sh_row of non-BVH kernels), the op counters, slack for the profiling build; the
-  // dynamic LDS holds the staged tables
-  const size_t static_lds = (size_t)block * (bvh ? 24 : 48) + 512 + (count ? 128 : 0);
+  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc; non-BVH
+  // kernels also the row totals sh_row and the bounce's throughput factor and ending radiance,
+  // sh_f / sh_le), the op counters, slack for the profiling build; the dynamic LDS holds the
+  // staged tables
+  const size_t static_lds = (size_t)block * (bvh ? 24 : 96) + 512 + (count ? 128 : 0);
   // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
   // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.
   const uint32_t used_perlins = sc->hdr.has_textures ? sc->hdr.n_perlins : 0u;
