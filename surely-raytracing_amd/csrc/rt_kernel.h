@@ -2159,18 +2159,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   __shared__ double sh_f[LDSF ? 3 * NB : 1];
   __shared__ double sh_le[LDSF ? 3 * NB : 1];
   const int tid = threadIdx.x;
-  // In-bounce camera rays (product non-BVH kernels, no defocus, max_depth >= 1): a lane whose
-  // sample ended at a miss or a light, and a lane that just claimed an item, takes its next camera
-  // ray inside the bounce instead of in a block of its own at the top of the next iteration. Its
-  // three draws of get_ray (render.rs:218-249: jitter x, jitter y, time; no defocus draws) are the
-  // three uniforms the scattering lanes draw in the shared shading block (the mixture coin or
-  // Schlick draw u0, then r1 and r2), in the same stream order, so a wave issues those draws once
-  // for both kinds of lanes; the camera ray is formed after the commit. A newly claimed lane traces
-  // one stale ray first (its bounce is dropped). Same rays, same images.
-  // (Not in VOL kernels: cornell_smoke ran 4.5 % slower with it, its path state spilling more;
-  // cornell_box gained 0.6 %, profiles/r04_ab3.log.)
-  constexpr bool CAMX_T = LDSF && !COUNT && !VOL;
-  const bool camx = CAMX_T && !kparams()->defocus && kparams()->max_depth > 0;
 
   d3 ro = mk(0., 0., 0.), rd = ro, beta = ro;
   double tm = 0.;
@@ -2310,7 +2298,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" ::"v"(ps.x), "v"(ps.y), "v"(ps.z), "v"(t2));
     }
 #endif
-    if (fresh && !camx) {
+    if (fresh) {
       const kparams_t Q = kparams();
       const int x = (int)(xk & 0xffffu);
       const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
@@ -2350,7 +2338,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // one back edge only (a `continue` here would give the loop header a second incoming state
     // and the compiler a full copy of it); a wave with no path in flight but more pools to
     // claim (a pool boundary) runs one bounce on stale rays, which the lanes then drop
-    if (!more && __ballot(alive | (camx & fresh)) == 0ull) break;
+    if (!more && __ballot(alive) == 0ull) break;
     // One bounce, run by EVERY lane of the wave (product kernels): a lane without a path (only
     // at the very end of a launch) traces its stale ray and its result is dropped below. The
     // scattered ray and throughput factor are committed unconditionally after the block, and
@@ -2365,7 +2353,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // and a zero-pdf bounce restarts the sum at 0), so its radiance is 0 until that bounce and
     // then 0 + beta * X = beta * X exactly: no running radiance is carried across bounces.
     bool term = false, emit_end = false;
-    bool cam = false;           // camx: the lane takes its next camera ray in this bounce
     d3 Le;                      // the ending lanes' radiance (undefined on the others)
     d3 p_next, d_next, f_next;  // the scattered ray and this bounce's throughput factor
     auto set_le = [&](d3 v) {
@@ -2411,24 +2398,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" ::"v"(t2), "v"(hn2), "v"(hf2), "v"(g2.s0));
     }
 #endif
-    const bool hitw = Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C);
-    if (!hitw) {
+    if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
       set_le(beta * karr3(kparams()->bg));
       term = emit_end = true;
-      if (!camx) break;  // camx: on to the sample's end below
+      break;
     }
-    // the hit record's values read by the shared shading block below; a camx lane that missed
-    // carries arbitrary (frozen, not undefined) values through it and a valid material pointer
-    d3 p = mk(__builtin_nondeterministic_value(0.), __builtin_nondeterministic_value(0.),
-              __builtin_nondeterministic_value(0.));
-    d3 normal = p;
-    bool front = true;
-    double u = 0., v = 0.;
-    TP M = T.mats;
-    uint4 mh;
-    uint32_t kind = __builtin_nondeterministic_value(0u);
-    if (hitw) {  // (always, unless camx)
     // ---- hit record of the winning primitive, recomputed in its own frame (deferred)
     PROF(2);
     const TP X = T.nodes + hn;
@@ -2443,9 +2418,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       asm volatile("" ::"v"(o2.x), "v"(o2.y), "v"(o2.z), "v"(d2.x), "v"(d2.y), "v"(d2.z));
     }
 #endif
-    p = vfma(t, d, o);
-    M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
-    mh = ld4u(M);
+    d3 p = vfma(t, d, o);
+    d3 normal;
+    bool front = true;
+    double u = 0., v = 0.;
+    const TP M = T.mats + (size_t)X[2] * RTL_MAT_WORDS;
+    uint4 mh = ld4u(M);
     const bool needs_uv = TEX && (mh.x & RTL_MATF_NEEDS_UV) != 0u;
     // the primitive's outward normal per type, then ONE set_face_normal (hittable.rs:22-37) for
     // every lane; a ConstantMedium hit has normal (1, 0, 0) and front_face true
@@ -2477,34 +2455,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     front = (type != RTL_QUAD && type != RTL_SPHERE) | (dot(d, outward) < 0.0);
     normal = front ? outward : -outward;
     Trav::frame_out(T.nodes, hf, p, normal);  // back to world space
-    kind = mh.x & 0xffu;
+    const uint32_t kind = mh.x & 0xffu;
     PROF(3);
     if ((SC & kScLight) && kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
       set_le(front ? beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C) : mk(0., 0., 0.));
       term = emit_end = true;
-      if (!camx) break;
+      break;
     }
-    }  // hitw
-    if constexpr (CAMX_T) {
-      if (camx) {
-        // the sample ended (miss, light): add its radiance now; a lane that goes on with its
-        // item (end_sample sets fresh), or that claimed one this iteration, seeds its next
-        // sample's stream here and draws its camera uniforms with the shading lanes below
-        if (term & alive) end_sample(mk(sh_le[tid], sh_le[NB + tid], sh_le[2 * NB + tid]));
-        cam = fresh;
-        if (cam) {
-          const kparams_t Q = kparams();
-          const int x = (int)(xk & 0xffffu);
-          const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
-          const int s_i = (int)(sij & 0xffffu), s_j = (int)((sij >> 16) & 0x7fffu);
-          g = rng_seed(Q->seed_lo, Q->seed_hi, (uint32_t)(y * Q->W + x),
-                       (uint32_t)(s_j * Q->sqrt_spp + s_i));
-        }
-        if (term & !cam) break;  // the lane's item is done: idle until its next claim
-      }
-    }
-    if ((SC & kScMetal) && !cam && kind == RT_MAT_METAL) {  // material.rs:124-134
+    if ((SC & kScMetal) && kind == RT_MAT_METAL) {  // material.rs:124-134
       C.inc(RT_OP_METAL);
       d3 reflected = reflect(unit_vector(rd), normal);
       d3 ruv = random_unit_vector(g);
@@ -2519,8 +2478,8 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // running two exclusive branches. Per lane the arithmetic and the draw order are exactly
     // those of the separate branches.
     PROF(4);
-    const bool diel = (SC & kScDielectric) && !cam && kind == RT_MAT_DIELECTRIC;
-    const bool iso = VOL && !cam && kind == RT_MAT_ISOTROPIC;  // VOL kernels: volumes or Isotropic
+    const bool diel = (SC & kScDielectric) && kind == RT_MAT_DIELECTRIC;
+    const bool iso = VOL && kind == RT_MAT_ISOTROPIC;  // VOL kernels: volumes or Isotropic
     C.inc(diel ? RT_OP_DIELECTRIC : (iso ? RT_OP_ISOTROPIC : RT_OP_LAMBERTIAN));
     // unit(r_in.direction) (material.rs:170) or CosinePDF's w = unit(normal) (pdf.rs:58-62)
     const d3 uu = unit_vector(diel ? rd : normal);
@@ -2542,18 +2501,16 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // first uniform: the Schlick test, drawn only when not TIR (material.rs:180), or the
     // mixture coin (pdf.rs:120-126)
     double u0 = 0.0;
-    if (cam || (diel ? !tir : have_lights)) u0 = rnd(g);
-    if (CAMX_T && camx) sh_le[tid] = u0;  // a camera lane's jitter x (render.rs:231)
+    if (diel ? !tir : have_lights) u0 = rnd(g);
     const double r0s = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
     // reflectance r0 + (1 - r0) * (1 - cos)^5 in the reference's operation order (material.rs:
     // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr)
     const bool refl = tir || r0s + (1.0 - r0s) * pow5_cr(1.0 - cos_t) > u0;
-    const bool light_branch = !diel && !cam && have_lights && u0 < 0.5;
+    const bool light_branch = !diel && have_lights && u0 < 0.5;
     d3 dir, factor;  // set on both arms below
     double cos_sl = cos_sl0;
     if (!diel) {
-      d3 atten = mk(0., 0., 0.);
-      if (!cam) atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
+      d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
       // Draw order as the reference: mixture coin (above), then light index
       // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
       uint32_t ltype = 0, li = 0;
@@ -2590,10 +2547,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         // and CosinePDF::generate (pdf.rs:75-77, vec3.rs:240-250) share one straight-line block:
         // one ONB, one sincos, selects instead of divergent branches.
         const double r1 = rnd(g), r2 = rnd(g);
-        if (CAMX_T && camx) {  // a camera lane's jitter y and time (render.rs:232, 240)
-          sh_le[NB + tid] = r1;
-          sh_le[2 * NB + tid] = r2;
-        }
         const bool lq = light_branch && ltype == RTL_QUAD;
         const bool ls = (SC & kScLSphere) && light_branch && ltype == RTL_SPHERE;
         d3 c = ls ? ld3(L, 0) : p;
@@ -2656,7 +2609,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       PROF(6);
       factor = atten * (s_pdf * rcp_w(pdf_val));
 #ifndef RT_ABL_NOXS  // ablation build: no special-value tracking (cost of RT_XS_*)
-      if (!cam && !(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
+      if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
         depth |= (int)((RT_XS_ON | xs_nan_bits(atten * s_pdf, beta)) << 24);
         beta = mk(1., 1., 1.);
         factor = beta;
@@ -2693,26 +2646,6 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         if (emit_end) Le = mk(sh_le[tid], sh_le[NB + tid], sh_le[2 * NB + tid]);
       }
       end_sample(emit_end ? Le : mk(0., 0., 0.));
-    }
-    if constexpr (CAMX_T) {
-      if (cam) {  // get_ray render.rs:218-249 from the uniforms drawn in the bounce
-        const kparams_t Q = kparams();
-        const int x = (int)(xk & 0xffffu);
-        const int y = Q->row_begin + (int)((xk >> 16) & 0x7fffu) * Q->row_step;
-        const int s_i = (int)(sij & 0xffffu), s_j = (int)((sij >> 16) & 0x7fffu);
-        d3 pc = vfma((double)y, karr3(Q->dv), vfma((double)x, karr3(Q->du), karr3(Q->p00)));
-        double px = fma(Q->rs, (double)s_i + sh_le[tid], -0.5);
-        double py = fma(Q->rs, (double)s_j + sh_le[NB + tid], -0.5);
-        d3 ps = pc + vfma(px, karr3(Q->du), karr3(Q->dv) * py);
-        const d3 origin = karr3(Q->center);
-        ro = origin;
-        rd = ps - origin;
-        tm = sh_le[2 * NB + tid];
-        beta = mk(1., 1., 1.);
-        depth = Q->max_depth;  // RT_XS_* cleared
-        alive = true;
-        fresh = false;
-      }
     }
   }
 #ifdef RT_PROF
