@@ -2151,7 +2151,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   __shared__ double sh_row[ROWS ? 3 * NB : 1];
   // Non-BVH kernels: a bounce's throughput factor and an ending path's radiance are set inside
   // the divergent shading branches and read after they join; held in registers across the join
-  // they were spilled to scratch at five waves per SIMD (cornell_smoke: 64 B per lane, three
+  // they were spilled to scratch at five waves per SIMD (cornell_smoke: 30 VGPRs, three
   // serialised scratch reloads per bounce, 35x the workspace's write bytes). Per-lane LDS slots
   // take the exec-masked writes of the branches as they are. (The BVH kernels' LDS holds the
   // compact trees; they keep registers, and do not spill there.)
