@@ -24,12 +24,12 @@ __global__ __launch_bounds__(256) void rt_gather_deinterleave_k(const float* __r
                                                                 float* __restrict__ frame,
                                                                 int row_floats, int height,
                                                                 int world, int max_rows) {
-  const int y = blockIdx.y;
-  if (y >= height) return;
-  const float* src = gathered + ((size_t)(y % world) * max_rows + y / world) * row_floats;
-  float* dst = frame + (size_t)y * row_floats;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
-    dst[i] = src[i];
+  for (int y = blockIdx.y; y < height; y += gridDim.y) {  // grid y is capped at 65535 rows
+    const float* src = gathered + ((size_t)(y % world) * max_rows + y / world) * row_floats;
+    float* dst = frame + (size_t)y * row_floats;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
+      dst[i] = src[i];
+  }
 }
 
 }  // namespace
@@ -101,7 +101,8 @@ int rt_gather_deinterleave(const float* gathered, int world, int width, int heig
   if (height == 0) return RT_OK;
   const int row_floats = width * 3;
   const int gx = (row_floats + 255) / 256 < 64 ? (row_floats + 255) / 256 : 64;
-  hipLaunchKernelGGL(rt_gather_deinterleave_k, dim3((unsigned)gx, (unsigned)height), dim3(256), 0,
+  const int gy = height < 65535 ? height : 65535;
+  hipLaunchKernelGGL(rt_gather_deinterleave_k, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0,
                      (hipStream_t)hip_stream, gathered, frame, row_floats, height, world,
                      rt_gather_max_rows(height, world));
   const hipError_t e = hipGetLastError();
