@@ -147,3 +147,22 @@ def test_scene_set_diagnostic_keeps_every_case(monkeypatch):
     blob, cam = rt.preset_blob("cornell_box", width=32, spp=4)
     state, src = rt.jit_check(blob)
     assert state == 1 and _scene_set(src) == 0xFFFFFFFF
+
+
+def test_code_object_cache_round_trip(tmp_path, monkeypatch):
+    """rt_jit.cpp's code-object cache (DESIGN §4.1b "Two compilers, one binary"): a compile with
+    RT_JIT_CACHE_WRITE=1 stores one object keyed by the generated source, the embedded headers and
+    the options; the same scene finds it (nothing rewritten); other options get a key of their own."""
+    monkeypatch.setenv("RT_JIT_CACHE_DIR", str(tmp_path))
+    monkeypatch.setenv("RT_JIT_CACHE_WRITE", "1")
+    monkeypatch.delenv("RT_JIT_OPTS", raising=False)
+    blob, _ = rt.preset_blob("cornell_box", width=16, spp=1)
+    assert rt.jit_check(blob)[0] == 1
+    files = sorted(tmp_path.glob("*.co"))
+    assert len(files) == 1 and files[0].stat().st_size > 1000
+    stamp = files[0].stat().st_mtime_ns
+    assert rt.jit_check(blob)[0] == 1
+    assert sorted(tmp_path.glob("*.co")) == files and files[0].stat().st_mtime_ns == stamp
+    monkeypatch.setenv("RT_JIT_OPTS", "-DRT_MIN_WAVES_GEN=4")
+    assert rt.jit_check(blob)[0] == 1
+    assert len(list(tmp_path.glob("*.co"))) == 2
