@@ -628,7 +628,8 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   // as far as the workgroup's LDS budget allows (the rest is read through the caches)
   P.bvh_words = sc->hdr.bvh_words;
   // Compact ordered BVHs (rt_layout.h CBVH) of a product render go to LDS after the staged
-  // tables, with the walk's per-lane u16 stacks (cbvh_walk); the reference BVH region then stays
+  // tables, with the walk's per-lane stacks (cbvh_walk: one u32 per tree level, header
+  // cbvh_stack bytes); the reference BVH region then stays
   // in global memory (only lanes flagged for the reference-order re-walk read it)
   P.cbvh_src = (const uint8_t*)(sc->nodes + sc->hdr.cbvh_word0);
   P.cbvh_bytes = sc->hdr.cbvh_words * 4u;
@@ -637,7 +638,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   size_t cbvh_lds = 0;
   {
     const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
-    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + (size_t)RTL_CBVH_STACK * block * 2;
+    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + (size_t)sc->hdr.cbvh_stack * block;
     if (bvh && !count && P.cbvh_bytes && !(opts->flags & RT_FLAG_REFERENCE_BVH) &&
         !std::getenv("RT_NO_CBVH_LDS") && need <= cap) {
       P.cbvh_lds_off = P.stage_bytes;

@@ -767,13 +767,13 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
     }
   }
   while (F.nodes.size() % 4) F.nodes.push_back(0u);
-  uint32_t cbvh_word0 = 0, cbvh_words = 0;
+  uint32_t cbvh_word0 = 0, cbvh_words = 0, cbvh_stack = 0;
   {  // ordered BVHs of the product kernels (rt_obvh.cpp), appended after the records
     std::vector<PrimBox> boxes(rec_words);
     for (auto& pb : em.pbox)
       if (pb.first < map.size() && map[pb.first] < rec_words) boxes[map[pb.first]] = pb.second;
     build_ordered_bvhs(F.nodes, rec_words, boxes, bvh_roots(F.nodes, root), &cbvh_word0,
-                       &cbvh_words);
+                       &cbvh_words, &cbvh_stack);
   }
   if (F.nodes.size() >= 0x7fffffffu) {
     *err = "scene too large";
@@ -851,6 +851,7 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   h.n_rec_words = rec_words;
   h.cbvh_word0 = cbvh_word0;
   h.cbvh_words = cbvh_words;
+  h.cbvh_stack = cbvh_stack;
   h.n_mats = (uint32_t)n_mat;
   h.n_texs = (uint32_t)n_tex;
   h.n_perlins = (uint32_t)n_perl;

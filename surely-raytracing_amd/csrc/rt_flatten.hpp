@@ -35,7 +35,7 @@ struct PrimBox {
 // its first word and size in words (0, 0 when there is none).
 void build_ordered_bvhs(std::vector<uint32_t>& nodes, uint32_t rec_words,
                         const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots,
-                        uint32_t* cbvh_word0, uint32_t* cbvh_words);
+                        uint32_t* cbvh_word0, uint32_t* cbvh_words, uint32_t* cbvh_stack);
 
 // Words of the node record starting with header word h (rt_layout.h).
 uint32_t record_words(uint32_t h);

@@ -1359,11 +1359,15 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   const lu4ptr nodes = reinterpret_cast<lu4ptr>(base);
   const lw_t refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
   const lw_t leaves = refs + n_int;
-  // the lane's stack entries are blockDim.x u16 apart; sp is kept as a byte offset (a step adds
-  // or subtracts sstep instead of multiplying an entry count by the stride)
-  typedef __attribute__((address_space(3))) uint16_t* ls_t;
-  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 2u * threadIdx.x;
-  const uint32_t sstep = 2u * blockDim.x;
+  // the lane's stack entries are blockDim.x u32 apart; sp is kept as a byte offset (a step adds
+  // or subtracts sstep instead of multiplying an entry count by the stride). An entry holds the
+  // pending child's reference (low 16 bits) and its box's entry time tn as bf16 (high 16 bits:
+  // f32 truncated, which rounds a tn >= 0 down; a negative tn is stored as -inf), so that a pop
+  // can drop a child whose box no longer passes against the CURRENT closest without reading its
+  // node (see pop below).
+  typedef __attribute__((address_space(3))) uint32_t* ls_t;
+  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 4u * threadIdx.x;
+  const uint32_t sstep = 4u * blockDim.x;
   auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
@@ -1410,6 +1414,25 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   constexpr uint32_t kDone = 0xffffu;
   uint32_t ref = hd.z & 0xffffu;
   uint32_t sp = 0;
+  auto entry = [](uint32_t child, float tn) {
+    return child | (tn < 0.0f ? 0xff800000u : (__float_as_uint(tn) & 0xffff0000u));
+  };
+  // Pop the next pending child, dropping those whose stored entry time tb fails box()'s test
+  // against the current closest: tb <= tn, tf <= close_f, and both sides of the test are
+  // monotone, so the child's box fails it, and so do its children's boxes (they lie inside it:
+  // entry times no earlier, the same f32 outward-rounded bounds) and a leaf's candidates (the
+  // margins that let box() cull a box keep every candidate <= closest (1 + kTieRel) inside its
+  // box). The walk visits the same nodes and leaves as with a full step per entry.
+  auto pop = [&]() -> uint32_t {
+    const float cut = fmaf(fabsf(close_f), kBoxRel, close_f);
+    while (sp > 0) {
+      sp -= sstep;
+      const uint32_t e = *slot(sp);
+      const float tb = __uint_as_float(e & 0xffff0000u);
+      if (!(fmaf(-fabsf(tb), kBoxRel, tb) > cut)) return e & 0xffffu;
+    }
+    return kDone;
+  };
 #ifdef RT_PROF  // profiling build: per-lane box steps / leaves, wave maxima, wave cycles (walk, leaves)
   uint32_t pf_box = 0, pf_leaf = 0;
   unsigned long long pf_leaf_cyc = 0;
@@ -1444,17 +1467,10 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
       // (A branch-free form -- the far child written to the free slot every step, the top read
       // speculatively before the box tests -- was 3.5 % slower at C4: r03_ab_cbvh_branchfree_c4.)
       if (h0 & h1) {  // both children hit: visit the nearer, push the other
-        *slot(sp) = (uint16_t)(first0 ? r1 : r0);
+        *slot(sp) = first0 ? entry(r1, tn1) : entry(r0, tn0);
         sp += sstep;
       }
-      if (h0 | h1) {
-        ref = first0 ? r0 : r1;
-      } else if (sp > 0) {
-        sp -= sstep;
-        ref = *slot(sp);
-      } else {
-        ref = kDone;
-      }
+      ref = (h0 | h1) ? (first0 ? r0 : r1) : pop();
 #ifdef RT_PROF
       ++pf_box;
 #endif
@@ -1480,12 +1496,7 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
 #ifdef RT_PROF
     pf_leaf_cyc += __builtin_readcyclecounter() - pf_l0;
 #endif
-    if (sp > 0) {
-      sp -= sstep;
-      ref = *slot(sp);
-    } else {
-      ref = kDone;
-    }
+    ref = pop();
   }
   flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
          (hit & (closest <= tmin * (1.0 + kTieRel)));

@@ -98,7 +98,8 @@
  *   tree: n_int internal nodes of 48 bytes (both children's boxes as f32 [lo_x hi_x lo_y hi_y
  *   lo_z hi_z], outward-rounded as above), n_int u32 child-reference pairs (ref0 | ref1 << 16;
  *   ref < 0x8000: internal node, else leaf index ref & 0x7fff), n_int + 1 u32 leaf records.
- *   Internal-node depth <= RTL_CBVH_STACK (the walk's per-lane stack).
+ *   Internal-node depth <= RTL_CBVH_STACK; the walk's per-lane LDS stack holds one u32 per
+ *   level of the deepest tree (child reference | bf16 entry time << 16), header cbvh_stack.
  * CBVH4 (A/B only, built with RT_CBVH4=1; header word 2 bit 31 set, bits 16-30 = n_int, bits
  *   0-15 = root reference): the same tree collapsed to 4 children per node (compact_tree4): n_int nodes of 96 bytes
  *   [lo_x 4][hi_x 4][lo_y 4][hi_y 4][lo_z 4][hi_z 4] (f32, child c in slot c; an empty slot is
@@ -179,4 +180,5 @@ typedef struct rtl_scene_header {
   uint32_t nested_volumes;/* a ConstantMedium lies inside another one's boundary      */
   uint32_t cbvh_word0;    /* CBVH region (below): first node word, 0 = none            */
   uint32_t cbvh_words;    /* its size in words (a multiple of 4)                        */
+  uint32_t cbvh_stack;    /* walk stack bytes per lane: 4 x the trees' largest depth     */
 } rtl_scene_header;

@@ -170,13 +170,14 @@ void f32_box(const BNode& n, float lo[3], float hi[3]) {
 // The compact copy of one tree (rt_layout.h CBVH) as words; false when it does not fit the
 // format (16-bit references, internal-node depth <= RTL_CBVH_STACK).
 bool compact_tree(const std::vector<BNode>& nodes, const std::vector<Leaf>& leaves,
-                  std::vector<uint32_t>* out, uint32_t* root_ref) {
+                  std::vector<uint32_t>* out, uint32_t* root_ref, int* depth) {
   const size_t n_leaf = leaves.size();
   if (n_leaf == 0 || n_leaf > 0x7fffu) return false;
   if (n_leaf == 1) {  // a single leaf: the root reference is the leaf
     out->assign(4, 0u);
     (*out)[0] = leaves[0].rec;
     *root_ref = 0x8000u;
+    *depth = 1;
     return true;
   }
   // internal nodes in pre-order (index 0 = the root), leaves in first-visit order
@@ -207,6 +208,7 @@ bool compact_tree(const std::vector<BNode>& nodes, const std::vector<Leaf>& leav
   wk.run(0, 1);
   const size_t n_int = order.size();
   if (n_int > 0x7fffu || max_depth > RTL_CBVH_STACK || leaf_recs.size() != n_leaf) return false;
+  *depth = max_depth;
   auto ref = [&](int c) -> uint32_t {
     return nodes[c].left < 0 ? 0x8000u | (uint32_t)leaf_of[c] : (uint32_t)int_of[c];
   };
@@ -328,9 +330,9 @@ bool compact_tree4(const std::vector<BNode>& nodes, const std::vector<Leaf>& lea
 
 void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
                         const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots,
-                        uint32_t* cbvh_word0, uint32_t* cbvh_words) {
+                        uint32_t* cbvh_word0, uint32_t* cbvh_words, uint32_t* cbvh_stack) {
   std::vector<uint32_t> cbvh;  // the compact region, appended after every ordered stream
-  *cbvh_word0 = *cbvh_words = 0u;
+  *cbvh_word0 = *cbvh_words = *cbvh_stack = 0u;
   for (uint32_t root : roots) {
     std::vector<Leaf> leaves;
     if (!collect(w, root, boxes, leaves, 0) || leaves.empty() || leaves.size() > (1u << 20))
@@ -394,12 +396,15 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
     // steps but tests more boxes and sorts them: 3.3 % slower at C4
     // (profiles/r03_ab_bvh4_vs_bvh2_c4.log)
     const bool four = std::getenv("RT_CBVH4") != nullptr;
-    if (!std::getenv("RT_NO_CBVH") &&
-        ((four && compact_tree4(B.nodes, leaves, &blk, &root_ref)) ||
-         compact_tree(B.nodes, leaves, &blk, &root_ref))) {
+    int depth = 0;
+    const bool as4 = four && compact_tree4(B.nodes, leaves, &blk, &root_ref);
+    if (!std::getenv("RT_NO_CBVH") && (as4 || compact_tree(B.nodes, leaves, &blk, &root_ref, &depth))) {
       w[hdr + 1] = (uint32_t)(cbvh.size() * 4);  // byte offset in the region
       w[hdr + 2] = root_ref;
       cbvh.insert(cbvh.end(), blk.begin(), blk.end());
+      // per-lane stack bytes: cbvh_walk keeps one u32 per level; cbvh4_walk RTL_CBVH_STACK u16
+      const uint32_t need = as4 ? 2u * RTL_CBVH_STACK : 4u * (uint32_t)depth;
+      *cbvh_stack = std::max(*cbvh_stack, need);
     }
   }
   if (!cbvh.empty()) {
