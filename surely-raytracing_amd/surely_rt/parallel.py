@@ -11,6 +11,9 @@ very different costs, and interleaving balances them. The RNG is keyed by the gl
 """
 from __future__ import annotations
 
+import ctypes as C
+from pathlib import Path
+
 import numpy as np
 
 
@@ -90,9 +93,6 @@ def gather_lib():
     one process per GPU without torch.distributed. Raises if it is not built."""
     global _gather
     if _gather is None:
-        import ctypes as C
-        from pathlib import Path
-
         path = Path(__file__).resolve().parent.parent.parent / "build" / "librtgather.so"
         if not path.exists():
             raise RuntimeError(f"{path} missing: run `make gather`")
@@ -120,8 +120,6 @@ class RcclFrameGather:
     """One rank's member of an RCCL communicator for the frame gather (rt_gather_comm)."""
 
     def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
-        import ctypes as C
-
         self._lib = gather_lib()
         h = C.c_void_p()
         rc = self._lib.rt_gather_comm_create(uid, world, rank, device, C.byref(h))
@@ -131,8 +129,6 @@ class RcclFrameGather:
 
     @staticmethod
     def unique_id() -> bytes:
-        import ctypes as C
-
         buf = C.create_string_buffer(128)
         lib = gather_lib()
         if lib.rt_gather_unique_id(buf) != 0:
@@ -141,8 +137,6 @@ class RcclFrameGather:
 
     def gather(self, local_ptr: int, width: int, height: int, scratch_ptr: int, frame_ptr: int,
                stream: int = 0):
-        import ctypes as C
-
         rc = self._lib.rt_gather_frame(self._h, C.c_void_p(local_ptr), width, height,
                                        C.c_void_p(scratch_ptr or None),
                                        C.c_void_p(frame_ptr or None), C.c_void_p(stream or None))
