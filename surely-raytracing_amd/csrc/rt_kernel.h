@@ -1387,13 +1387,20 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   double closest = tmax;
   float close_f = (float)(closest + closest * (2.0 * kTieRel));
   bool hit = false;
-  double tie_at = -1.0;
+  // The tie flag from the two smallest values of {tmax, every candidate}: `closest` is the
+  // smallest, `second` the next. obvh_walk flags a lane when a candidate came within kTieRel of
+  // the running closest and that closest is within 2 kTieRel of the final one; any such pair
+  // (the running closest a, the candidate b) makes the two smallest values lie within
+  // 2 kTieRel (+ roundings) of each other, so testing second <= closest (1 + 3 kTieRel) flags
+  // every lane obvh_walk flags (and at most a few more, which re-walk in the reference order).
+  // A candidate then costs a min, a max and the winner's selects, not the tie test's four.
+  double second = kInf;
   uint32_t hn = 0;
   auto cand = [&](bool valid, double t, uint32_t rec) {
-    const bool nt = valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel);
-    tie_at = nt ? closest : tie_at;
-    const bool win = valid & (t < closest);
-    closest = win ? t : closest;
+    const double te = valid ? t : kInf;
+    second = fmin(second, fmax(closest, te));
+    const bool win = te < closest;
+    closest = win ? te : closest;
     hn = win ? rec : hn;
     hit = hit | win;
   };
@@ -1498,7 +1505,7 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
 #endif
     ref = pop();
   }
-  flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
+  flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
          (hit & (closest <= tmin * (1.0 + kTieRel)));
 #ifdef RT_PROF
   {
