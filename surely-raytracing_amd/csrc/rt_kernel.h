@@ -1209,7 +1209,8 @@ __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d
         const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
         inr = !(lo < 0.0) & !(1.0 < hi);
       }
-      cand(!(fabs(dk) < 1e-8) & (tmin <= t) & (t < kInf) & inr, t, qrec);
+      // (a t of +inf needs no test of its own: no walker's candidate logic can take it)
+      cand(!(fabs(dk) < 1e-8) & (tmin <= t) & inr, t, qrec);
     }
   }
 }
