@@ -1542,149 +1542,6 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   return hit;
 }
 
-// The walk over the 4-wide compact tree (rt_layout.h CBVH4). A step reads the node's near and
-// far bound for each axis as four-child blocks (the lane's octant picks which stored block is
-// near, so no per-child select), tests the four child boxes with cbvh_walk's arithmetic (the
-// same f32 bounds, the same culling margins), sorts them by entry time, visits the nearest hit
-// child and pushes the other hit children so that they pop nearest first. Candidates and tie
-// flags are obvh_walk's, so the result is the same closest candidate and the same flag.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-template <bool MAIN>
-__device__ bool cbvh4_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm, int frame,
-                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
-                           int& hit_frame, bool& flag) {
-  typedef const __attribute__((address_space(3))) uint8_t* lb_t;
-  typedef __attribute__((address_space(3))) uint8_t* lbw_t;
-  typedef const __attribute__((address_space(3))) uint32_t* lw_t;
-  typedef const __attribute__((address_space(3))) f32x4* l4f_t;
-  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-  typedef const __attribute__((address_space(3))) v2u* l2u_t;
-  typedef __attribute__((address_space(3))) uint16_t* ls_t;
-  const gptr N = (gptr)P.nodes;
-  const uint32_t n_int = (hd.z >> 16) & 0x7fffu;
-  const lb_t base = (lb_t)rt_lds + P.cbvh_lds_off + hd.y;
-  const lb_t refs = base + n_int * 96u;
-  const lw_t leaves = reinterpret_cast<lw_t>(refs + n_int * 8u);
-  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 2u * threadIdx.x;
-  const uint32_t sstep = 2u * blockDim.x;
-  auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
-  const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
-  const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
-  // byte offsets of the near / far bound blocks per axis in a node (d_a < 0: hi is near)
-  const uint32_t onx = nx ? 16u : 0u, ofx = 16u - onx;
-  const uint32_t ony = ny ? 48u : 32u, ofy = 80u - ony;
-  const uint32_t onz = nz ? 80u : 64u, ofz = 144u - onz;
-  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
-  constexpr float kBoxRel = 0x1p-20f;
-  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
-  const f32x2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
-  const f32x2 ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
-  const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
-  double closest = tmax;
-  float close_f = (float)(closest + closest * (2.0 * kTieRel));
-  bool hit = false;
-  double tie_at = -1.0;
-  uint32_t hn = 0;
-  auto cand = [&](bool valid, double t, uint32_t rec) {
-    const bool nt = valid & (closest < kInf) & (fabs(t - closest) <= closest * kTieRel);
-    tie_at = nt ? closest : tie_at;
-    const bool win = valid & (t < closest);
-    closest = win ? t : closest;
-    hn = win ? rec : hn;
-    hit = hit | win;
-  };
-  // one child's slab test from its per-axis near / far slab times (cbvh_walk's box())
-  auto pass = [&](float tnx, float tfx, float tny, float tfy, float tnz, float tfz, float& key) {
-    const float tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
-    const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
-    const bool h = fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
-    key = h ? tn : __builtin_inff();  // a box that passes has a finite entry time
-  };
-  constexpr uint32_t kDone = 0xffffu;
-  uint32_t ref = hd.z & 0xffffu;
-  uint32_t sp = 0;
-  for (;;) {
-    while (ref < 0x8000u) {
-      const lb_t nb = base + ref * 96u;
-      const f32x4 NX = *reinterpret_cast<l4f_t>(nb + onx), FX = *reinterpret_cast<l4f_t>(nb + ofx);
-      const f32x4 NY = *reinterpret_cast<l4f_t>(nb + ony), FY = *reinterpret_cast<l4f_t>(nb + ofy);
-      const f32x4 NZ = *reinterpret_cast<l4f_t>(nb + onz), FZ = *reinterpret_cast<l4f_t>(nb + ofz);
-      const v2u rr = *reinterpret_cast<l2u_t>(refs + ref * 8u);
-      // slab times, two children per packed f32 subtract and multiply
-      const f32x2 nx01 = (f32x2{NX.x, NX.y} - ox2) * ix2, nx23 = (f32x2{NX.z, NX.w} - ox2) * ix2;
-      const f32x2 fx01 = (f32x2{FX.x, FX.y} - ox2) * ix2, fx23 = (f32x2{FX.z, FX.w} - ox2) * ix2;
-      const f32x2 ny01 = (f32x2{NY.x, NY.y} - oy2) * iy2, ny23 = (f32x2{NY.z, NY.w} - oy2) * iy2;
-      const f32x2 fy01 = (f32x2{FY.x, FY.y} - oy2) * iy2, fy23 = (f32x2{FY.z, FY.w} - oy2) * iy2;
-      const f32x2 nz01 = (f32x2{NZ.x, NZ.y} - oz2) * iz2, nz23 = (f32x2{NZ.z, NZ.w} - oz2) * iz2;
-      const f32x2 fz01 = (f32x2{FZ.x, FZ.y} - oz2) * iz2, fz23 = (f32x2{FZ.z, FZ.w} - oz2) * iz2;
-      float k0, k1, k2, k3;
-      pass(nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, k0);
-      pass(nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y, k1);
-      pass(nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x, k2);
-      pass(nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y, k3);
-      uint32_t c0 = rr.x & 0xffffu, c1 = rr.x >> 16, c2 = rr.y & 0xffffu, c3 = rr.y >> 16;
-      // sort the four (entry time, child) pairs ascending; missed children sort last (+inf)
-      auto cas = [](float& ka, uint32_t& ca, float& kb, uint32_t& cb) {
-        const bool sw = kb < ka;
-        const float k = ka;
-        const uint32_t c = ca;
-        ka = sw ? kb : ka;
-        ca = sw ? cb : ca;
-        kb = sw ? k : kb;
-        cb = sw ? c : cb;
-      };
-      cas(k0, c0, k1, c1);
-      cas(k2, c2, k3, c3);
-      cas(k0, c0, k2, c2);
-      cas(k1, c1, k3, c3);
-      cas(k1, c1, k2, c2);
-      constexpr float kI = __builtin_inff();
-      // the other hit children, farthest first, so the next nearest is on top
-      if (k3 < kI) {
-        *slot(sp) = (uint16_t)c3;
-        sp += sstep;
-      }
-      if (k2 < kI) {
-        *slot(sp) = (uint16_t)c2;
-        sp += sstep;
-      }
-      if (k1 < kI) {
-        *slot(sp) = (uint16_t)c1;
-        sp += sstep;
-      }
-      if (k0 < kI) {
-        ref = c0;
-      } else if (sp > 0) {
-        sp -= sstep;
-        ref = *slot(sp);
-      } else {
-        ref = kDone;
-      }
-    }
-    if (ref == kDone) break;
-    const double closest_before = closest;
-    obvh_leaf(N, leaves[ref & 0x7fffu], o, d, r, tm, tmin, cand);
-    if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
-    if (sp > 0) {
-      sp -= sstep;
-      ref = *slot(sp);
-    } else {
-      ref = kDone;
-    }
-  }
-  flag = ((tie_at >= 0.0) & (fabs(tie_at - closest) <= closest * (2.0 * kTieRel))) |
-         (hit & (closest <= tmin * (1.0 + kTieRel)));
-  if (hit) {
-    t_out = closest;
-    if (MAIN) {
-      hit_node = hn;
-      hit_frame = frame;
-    }
-  }
-  return hit;
-}
-
 template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
@@ -1701,10 +1558,7 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
     asm volatile("" : "+v"(z));
     const uint4 hd2 = ld4u((gptr)P.nodes + obvh);
     const bool h2 = (P.cbvh_lds_off != ~0u && hd2.y != ~0u)
-                        ? ((hd2.z >> 31) ? cbvh4_walk<MAIN>(P, hd2, o, d, tm, frame, tmin + z, tmax,
-                                                            t2, hn2, hf2, f2)
-                                         : cbvh_walk<MAIN>(P, hd2, o, d, tm, frame, tmin + z, tmax,
-                                                           t2, hn2, hf2, f2))
+                        ? cbvh_walk<MAIN>(P, hd2, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2)
                         : obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin + z, tmax, t2, hn2, hf2, f2);
     asm volatile("" ::"v"(t2), "v"(hn2), "v"(h2), "v"(f2));
   }
@@ -1714,11 +1568,8 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
       bool flag = false;
       const uint4 hd = ld4u((gptr)P.nodes + obvh);  // [n_entries][cbvh block][root ref][streams]
       bool h;
-      if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS (4- or 2-wide)
-        h = (hd.z >> 31) ? cbvh4_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node,
-                                            hit_frame, flag)
-                         : cbvh_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node,
-                                           hit_frame, flag);
+      if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
+        h = cbvh_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
       else
         h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,
                             flag);

@@ -100,11 +100,7 @@
  *   ref < 0x8000: internal node, else leaf index ref & 0x7fff), n_int + 1 u32 leaf records.
  *   Internal-node depth <= RTL_CBVH_STACK; the walk's per-lane LDS stack holds one u32 per
  *   level of the deepest tree (child reference | bf16 entry time << 16), header cbvh_stack.
- * CBVH4 (A/B only, built with RT_CBVH4=1; header word 2 bit 31 set, bits 16-30 = n_int, bits
- *   0-15 = root reference): the same tree collapsed to 4 children per node (compact_tree4): n_int nodes of 96 bytes
- *   [lo_x 4][hi_x 4][lo_y 4][hi_y 4][lo_z 4][hi_z 4] (f32, child c in slot c; an empty slot is
- *   the empty box +inf..-inf), n_int x 4 u16 child references (0xffff = empty), n_leaf u32 leaf
- *   records. At most RTL_CBVH_STACK children pending on the walk's stack. */
+ */
 #define RTL_CBVH_STACK 32
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):

@@ -233,101 +233,6 @@ bool compact_tree(const std::vector<BNode>& nodes, const std::vector<Leaf>& leav
   return true;
 }
 
-// The compact copy as a 4-wide tree (rt_layout.h CBVH4): the BVH2 collapsed greedily (a node
-// takes its children and, while it has fewer than four, opens its largest-area internal child),
-// so a walk step tests up to four child boxes and a walk takes about half the steps. The child
-// boxes are the BVH2's own nodes' boxes (the same outward-rounded f32 bounds), so every box test
-// is one the BVH2 walk could make. False when the tree does not fit the format (16-bit
-// references, a stack of at most RTL_CBVH_STACK pending children).
-bool compact_tree4(const std::vector<BNode>& nodes, const std::vector<Leaf>& leaves,
-                   std::vector<uint32_t>* out, uint32_t* root_word) {
-  const size_t n_leaf = leaves.size();
-  if (n_leaf == 0 || n_leaf > 0x7fffu) return false;
-  if (n_leaf == 1) {
-    out->assign(4, 0u);
-    (*out)[0] = leaves[0].rec;
-    *root_word = 0x8000u | 0x80000000u;
-    return true;
-  }
-  struct N4 {
-    int child[4];  // BVH2 node indices, -1 = empty slot
-  };
-  std::vector<N4> n4;
-  std::vector<int> leaf_of(nodes.size(), -1);
-  std::vector<uint32_t> leaf_recs;
-  std::vector<std::vector<int>> kids;  // per BVH4 node: its children as BVH2 indices
-  int max_stack = 0;
-  struct Collapse {
-    const std::vector<BNode>& N;
-    const std::vector<Leaf>& L;
-    std::vector<std::vector<int>>& kids;
-    std::vector<int>& leaf_of;
-    std::vector<uint32_t>& recs;
-    int& max_stack;
-    std::vector<int> id_of;  // BVH2 internal node -> BVH4 node index
-    int run(int i, int pending) {  // returns the BVH4 index of BVH2 internal node i
-      std::vector<int> c = {N[i].left, N[i].right};
-      while (c.size() < 4) {
-        int best = -1;
-        double best_a = -1.0;
-        for (size_t k = 0; k < c.size(); ++k)
-          if (N[c[k]].left >= 0) {
-            const double a = area(N[c[k]].lo, N[c[k]].hi);
-            if (a > best_a) best_a = a, best = (int)k;
-          }
-        if (best < 0) break;
-        const int o = c[best];
-        c[best] = N[o].left;
-        c.insert(c.begin() + best + 1, N[o].right);
-      }
-      const int id = (int)kids.size();
-      kids.push_back(c);
-      id_of[i] = id;
-      const int p = pending + (int)c.size() - 1;  // siblings still on the stack below a child
-      max_stack = std::max(max_stack, p);
-      for (int k : c) {
-        if (N[k].left < 0) {
-          leaf_of[k] = (int)recs.size();
-          recs.push_back(L[N[k].right].rec);
-        } else {
-          run(k, p);
-        }
-      }
-      return id;
-    }
-  } col{nodes, leaves, kids, leaf_of, leaf_recs, max_stack, std::vector<int>(nodes.size(), -1)};
-  col.run(0, 0);
-  const size_t n_int = kids.size();
-  if (n_int > 0x7fffu || max_stack > RTL_CBVH_STACK || leaf_recs.size() != n_leaf) return false;
-  auto ref = [&](int c) -> uint32_t {
-    return nodes[c].left < 0 ? 0x8000u | (uint32_t)leaf_of[c] : (uint32_t)col.id_of[c];
-  };
-  const size_t words = (n_int * 24 + n_int * 2 + n_leaf + 3) & ~(size_t)3;
-  out->assign(words, 0u);
-  uint32_t* B = out->data();
-  const float pinf = HUGE_VALF, ninf = -HUGE_VALF;
-  for (size_t k = 0; k < n_int; ++k) {
-    uint32_t* nd = B + k * 24;  // [lo_x 4][hi_x 4][lo_y 4][hi_y 4][lo_z 4][hi_z 4]
-    uint16_t rf[4] = {0xffffu, 0xffffu, 0xffffu, 0xffffu};
-    for (int c = 0; c < 4; ++c) {
-      float lo[3] = {pinf, pinf, pinf}, hi[3] = {ninf, ninf, ninf};  // empty slot: never hit
-      if (c < (int)kids[k].size()) {
-        f32_box(nodes[kids[k][c]], lo, hi);
-        rf[c] = (uint16_t)ref(kids[k][c]);
-      }
-      for (int a = 0; a < 3; ++a) {
-        std::memcpy(&nd[8 * a + c], &lo[a], 4);
-        std::memcpy(&nd[8 * a + 4 + c], &hi[a], 4);
-      }
-    }
-    B[n_int * 24 + 2 * k] = rf[0] | (uint32_t)rf[1] << 16;
-    B[n_int * 24 + 2 * k + 1] = rf[2] | (uint32_t)rf[3] << 16;
-  }
-  for (size_t k = 0; k < n_leaf; ++k) B[n_int * 26 + k] = leaf_recs[k];
-  *root_word = 0u | (uint32_t)n_int << 16 | 0x80000000u;
-  return true;
-}
-
 void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
                         const std::vector<PrimBox>& boxes, const std::vector<uint32_t>& roots,
                         uint32_t* cbvh_word0, uint32_t* cbvh_words, uint32_t* cbvh_stack) {
@@ -392,19 +297,15 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
     std::vector<uint32_t> blk;
     uint32_t root_ref = 0u;
     w[hdr + 1] = 0xffffffffu;
-    // the two-wide compact tree; RT_CBVH4=1 (A/B) the 4-wide one, which walks in about half the
-    // steps but tests more boxes and sorts them: 3.3 % slower at C4
-    // (profiles/r03_ab_bvh4_vs_bvh2_c4.log)
-    const bool four = std::getenv("RT_CBVH4") != nullptr;
+    // the two-wide compact tree (a 4-wide form walked in about half the steps but tested more
+    // boxes and sorted them: 3.3 % slower at C4, profiles/r03_ab_bvh4_vs_bvh2_c4.log; removed)
     int depth = 0;
-    const bool as4 = four && compact_tree4(B.nodes, leaves, &blk, &root_ref);
-    if (!std::getenv("RT_NO_CBVH") && (as4 || compact_tree(B.nodes, leaves, &blk, &root_ref, &depth))) {
+    if (!std::getenv("RT_NO_CBVH") && compact_tree(B.nodes, leaves, &blk, &root_ref, &depth)) {
       w[hdr + 1] = (uint32_t)(cbvh.size() * 4);  // byte offset in the region
       w[hdr + 2] = root_ref;
       cbvh.insert(cbvh.end(), blk.begin(), blk.end());
-      // per-lane stack bytes: cbvh_walk keeps one u32 per level; cbvh4_walk RTL_CBVH_STACK u16
-      const uint32_t need = as4 ? 2u * RTL_CBVH_STACK : 4u * (uint32_t)depth;
-      *cbvh_stack = std::max(*cbvh_stack, need);
+      // per-lane stack bytes: cbvh_walk keeps one u32 per tree level
+      *cbvh_stack = std::max(*cbvh_stack, 4u * (uint32_t)depth);
     }
   }
   if (!cbvh.empty()) {

@@ -73,13 +73,12 @@ def test_ordered_bvhs_for_primitive_leaf_subtrees():
     assert st["bvh_records"] > 0 and st["ordered_bvhs"] == 0
 
 
-def test_compact_bvhs_fit_the_lds_budget(monkeypatch):
+def test_compact_bvhs_fit_the_lds_budget():
     """rt_obvh.cpp / rt_layout.h CBVH: both final_scene trees also get the compact copy that
     cbvh_walk reads from LDS (48-byte two-child nodes, u16 references), and with the per-lane
     stacks of a 768-thread workgroup (one u32 per tree level: final_scene's trees are 10 and 12
     levels deep, so at most 16 x 4 bytes), the f64 sample sums and the Perlin table it fits the
-    CU's 160 KiB. RT_CBVH4=1 (A/B only) builds the 4-wide form (CBVH4: 96-byte
-    four-child nodes, 4 u16 references), which must fit as well."""
+    CU's 160 KiB."""
     blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
     st = rt.layout_stats(blob)
     assert st["compact_bvhs"] == st["ordered_bvhs"] == 2
@@ -88,10 +87,3 @@ def test_compact_bvhs_fit_the_lds_budget(monkeypatch):
     assert n_int * 52 + n_leaves * 4 <= st["compact_bvh_bytes"] <= n_int * 52 + n_leaves * 4 + 32
     stacks, sums, perlin = 16 * 768 * 4, 768 * 24, 8960
     assert st["compact_bvh_bytes"] + stacks + sums + perlin + 512 <= 160 * 1024
-    monkeypatch.setenv("RT_CBVH4", "1")
-    st4 = rt.layout_stats(blob)
-    # a 4-wide node holds 2-4 children: n_leaves - 1 <= 3 n_int4 and n_int4 <= n_leaves - 1
-    lo = (n_leaves + 1) // 3 * 104 + n_leaves * 4
-    assert st4["compact_bvhs"] == 2
-    assert lo <= st4["compact_bvh_bytes"] <= n_int * 104 + n_leaves * 4 + 32
-    assert st4["compact_bvh_bytes"] + stacks + sums + perlin + 512 <= 160 * 1024
