@@ -1347,8 +1347,12 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
 // the order of the steps and where the nodes come from differ. The LDS copy turns the walk's
 // dependent L2 round trips (~1 us each, the kernel waited on memory about half its cycles) into
 // LDS reads, and a step covers two boxes.
-template <bool MAIN>
-__device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm, int frame,
+// TPOS (tmin >= 0, every walk but a ConstantMedium boundary's): entry times are then >= 0 and a
+// box passes when tn <= tf * kBoxPos, one product for box()'s two widenings. It keeps every box
+// the widened test keeps: that test passing means tn (1 - 2^-20)(1 - u) <= tf (1 + 2^-20)(1 + u)
+// (u = 2^-24, one rounding each), i.e. tn <= tf (1 + 2^-19 + 2u + ...) <= fl(tf * kBoxPos).
+template <bool MAIN, bool TPOS>
+__device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm, int frame,
                           double tmin, double tmax, double& t_out, uint32_t& hit_node,
                           int& hit_frame, bool& flag) {
   typedef const __attribute__((address_space(3))) uint8_t* lb_t;
@@ -1374,6 +1378,7 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
   constexpr float kBoxRel = 0x1p-20f;
+  constexpr float kBoxPos = 1.0f + 0x1p-18f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
   // slab times as fma(bound, inv, -o inv): one packed fma per axis instead of a subtraction and
@@ -1417,7 +1422,11 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
     const float tnz = nz ? tz2.y : tz2.x, tfz = nz ? tz2.x : tz2.y;
     tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
     const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
-    return fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
+    if constexpr (TPOS) {
+      return tn <= tf * kBoxPos;
+    } else {
+      return fmaf(-fabsf(tn), kBoxRel, tn) <= fmaf(fabsf(tf), kBoxRel, tf);
+    }
   };
   constexpr uint32_t kDone = 0xffffu;
   uint32_t ref = hd.z & 0xffffu;
@@ -1432,12 +1441,13 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
   // margins that let box() cull a box keep every candidate <= closest (1 + kTieRel) inside its
   // box). The walk visits the same nodes and leaves as with a full step per entry.
   auto pop = [&]() -> uint32_t {
-    const float cut = fmaf(fabsf(close_f), kBoxRel, close_f);
+    const float cut = TPOS ? close_f * kBoxPos : fmaf(fabsf(close_f), kBoxRel, close_f);
     while (sp > 0) {
       sp -= sstep;
       const uint32_t e = *slot(sp);
       const float tb = __uint_as_float(e & 0xffff0000u);
-      if (!(fmaf(-fabsf(tb), kBoxRel, tb) > cut)) return e & 0xffffu;
+      const bool drop = TPOS ? (tb > cut) : (fmaf(-fabsf(tb), kBoxRel, tb) > cut);
+      if (!drop) return e & 0xffffu;
     }
     return kDone;
   };
@@ -1540,6 +1550,15 @@ __device__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
     }
   }
   return hit;
+}
+template <bool MAIN>
+__device__ __forceinline__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, d3 d, double tm,
+                                          int frame, double tmin, double tmax, double& t_out,
+                                          uint32_t& hit_node, int& hit_frame, bool& flag) {
+  return tmin >= 0.0 ? cbvh_walk_t<MAIN, true>(P, hd, o, d, tm, frame, tmin, tmax, t_out,
+                                               hit_node, hit_frame, flag)
+                     : cbvh_walk_t<MAIN, false>(P, hd, o, d, tm, frame, tmin, tmax, t_out,
+                                                hit_node, hit_frame, flag);
 }
 
 template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
