@@ -1361,7 +1361,6 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
   const gptr N = (gptr)P.nodes;
   const uint32_t n_int = (hd.x - 1u) >> 1;  // n_entries = 2 n_leaf - 1
   const lb_t base = (lb_t)rt_lds + P.cbvh_lds_off + hd.y;
-  const lu4ptr nodes = reinterpret_cast<lu4ptr>(base);
   const lw_t refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
   const lw_t leaves = refs + n_int;
   // the lane's stack entries are blockDim.x u32 apart; sp is kept as a byte offset (a step adds
@@ -1412,14 +1411,13 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
   };
   // slab test of one child box [lo_x hi_x lo_y hi_y lo_z hi_z]: the octant's near bound per axis
   // is hi where d_a < 0, as in the OBVH streams
-  auto box = [&](float lx, float hx, float ly, float hy, float lz, float hz, float& tn) {
-    const f32x2 bx = {lx, hx}, by = {ly, hy}, bz = {lz, hz};
-    const f32x2 tx2 = __builtin_elementwise_fma(bx, ix2, nox2),
-                ty2 = __builtin_elementwise_fma(by, iy2, noy2),
-                tz2 = __builtin_elementwise_fma(bz, iz2, noz2);
-    const float tnx = nx ? tx2.y : tx2.x, tfx = nx ? tx2.x : tx2.y;
-    const float tny = ny ? ty2.y : ty2.x, tfy = ny ? ty2.x : ty2.y;
-    const float tnz = nz ? tz2.y : tz2.x, tfz = nz ? tz2.x : tz2.y;
+  // A node stores each axis's bounds as [lo c0, lo c1, hi c0, hi c1] (rt_layout.h CBVH): the
+  // lane reads its octant's near pair and far pair of both children with one 8-byte load each at
+  // a per-lane byte offset, and forms both children's slab times of an axis with one packed fma
+  // (no per-child select).
+  typedef const __attribute__((address_space(3))) f32x2* lf2_t;
+  const uint32_t onx = nx ? 8u : 0u, ony = ny ? 24u : 16u, onz = nz ? 40u : 32u;
+  auto box = [&](float tnx, float tfx, float tny, float tfy, float tnz, float tfz, float& tn) {
     tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
     const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
     if constexpr (TPOS) {
@@ -1473,13 +1471,17 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
         break;
       }
 #endif
-      const v4u a = nodes[3 * ref], b = nodes[3 * ref + 1], c = nodes[3 * ref + 2];
+      const lb_t nb = base + ref * 48u;
+      const f32x2 NX = *reinterpret_cast<lf2_t>(nb + onx), FX = *reinterpret_cast<lf2_t>(nb + (onx ^ 8u));
+      const f32x2 NY = *reinterpret_cast<lf2_t>(nb + ony), FY = *reinterpret_cast<lf2_t>(nb + (ony ^ 8u));
+      const f32x2 NZ = *reinterpret_cast<lf2_t>(nb + onz), FZ = *reinterpret_cast<lf2_t>(nb + (onz ^ 8u));
       const uint32_t rr = refs[ref];
+      const f32x2 tnx = __builtin_elementwise_fma(NX, ix2, nox2), tfx = __builtin_elementwise_fma(FX, ix2, nox2);
+      const f32x2 tny = __builtin_elementwise_fma(NY, iy2, noy2), tfy = __builtin_elementwise_fma(FY, iy2, noy2);
+      const f32x2 tnz = __builtin_elementwise_fma(NZ, iz2, noz2), tfz = __builtin_elementwise_fma(FZ, iz2, noz2);
       float tn0, tn1;
-      const bool h0 = box(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z),
-                          __uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y), tn0);
-      const bool h1 = box(__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x),
-                          __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w), tn1);
+      const bool h0 = box(tnx.x, tfx.x, tny.x, tfy.x, tnz.x, tfz.x, tn0);
+      const bool h1 = box(tnx.y, tfx.y, tny.y, tfy.y, tnz.y, tfz.y, tn1);
       const bool first0 = h0 & (!h1 | (tn0 <= tn1));
       const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
       // (A branch-free form -- the far child written to the free slot every step, the top read

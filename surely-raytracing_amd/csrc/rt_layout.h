@@ -95,8 +95,10 @@
  *   none) and its root reference.
  * CBVH: the same trees, compact, for the walk from LDS (rt_kernel.h cbvh_walk): one contiguous
  *   region after the OBVHs (header cbvh_word0 / cbvh_words) of 16-byte aligned blocks, one per
- *   tree: n_int internal nodes of 48 bytes (both children's boxes as f32 [lo_x hi_x lo_y hi_y
- *   lo_z hi_z], outward-rounded as above), n_int u32 child-reference pairs (ref0 | ref1 << 16;
+ *   tree: n_int internal nodes of 48 bytes (both children's boxes as f32, outward-rounded as
+ *   above, blocked per axis: [lo_x c0, lo_x c1, hi_x c0, hi_x c1, lo_y c0, ..., hi_z c1], so a
+ *   lane reads its octant's near and far pair of an axis with one 8-byte load each), n_int u32
+ *   child-reference pairs (ref0 | ref1 << 16;
  *   ref < 0x8000: internal node, else leaf index ref & 0x7fff), n_int + 1 u32 leaf records.
  *   Internal-node depth <= RTL_CBVH_STACK; the walk's per-lane LDS stack holds one u32 per
  *   level of the deepest tree (child reference | bf16 entry time << 16), header cbvh_stack.

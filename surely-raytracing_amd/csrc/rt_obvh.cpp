@@ -221,9 +221,10 @@ bool compact_tree(const std::vector<BNode>& nodes, const std::vector<Leaf>& leav
     for (int c = 0; c < 2; ++c) {
       float lo[3], hi[3];
       f32_box(nodes[ch[c]], lo, hi);
+      // per axis a: [lo_a child 0, lo_a child 1, hi_a child 0, hi_a child 1] (rt_layout.h CBVH)
       for (int a = 0; a < 3; ++a) {
-        std::memcpy(&B[k * 12 + c * 6 + 2 * a], &lo[a], 4);
-        std::memcpy(&B[k * 12 + c * 6 + 2 * a + 1], &hi[a], 4);
+        std::memcpy(&B[k * 12 + 4 * a + c], &lo[a], 4);
+        std::memcpy(&B[k * 12 + 4 * a + 2 + c], &hi[a], 4);
       }
     }
     B[n_int * 12 + k] = ref(n.left) | ref(n.right) << 16;
