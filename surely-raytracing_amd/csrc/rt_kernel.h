@@ -1482,15 +1482,22 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
       float tn0, tn1;
       const bool h0 = box(tnx.x, tfx.x, tny.x, tfy.x, tnz.x, tfz.x, tn0);
       const bool h1 = box(tnx.y, tfx.y, tny.y, tfy.y, tnz.y, tfz.y, tn1);
-      const bool first0 = h0 & (!h1 | (tn0 <= tn1));
+      // Logical (not bitwise) operators on the hit flags: `h0 & h1` on bools is int arithmetic,
+      // which the compiler kept as 0/1 values in VGPRs (two v_cndmask, two v_and and a v_cmp per
+      // step); with && / || the flags stay lane masks in SGPRs (C4 -2.7 %, r04_ab16_c4_steps.log).
+      const bool first0 = h0 && (!h1 || (tn0 <= tn1));
       const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
-      // (A branch-free form -- the far child written to the free slot every step, the top read
-      // speculatively before the box tests -- was 3.5 % slower at C4: r03_ab_cbvh_branchfree_c4.)
-      if (h0 & h1) {  // both children hit: visit the nearer, push the other
-        *slot(sp) = first0 ? entry(r1, tn1) : entry(r0, tn0);
-        sp += sstep;
-      }
-      ref = (h0 | h1) ? (first0 ? r0 : r1) : pop();
+      const bool any = h0 || h1;
+      const uint32_t nref = first0 ? r0 : r1;
+      // Both children hit: visit the nearer, push the other. The far entry is written to the
+      // free slot every step and kept (sp advanced) only then: no branch around the store. The
+      // slot is inside the lane's stack: at an internal node of depth k the stack holds at most
+      // k - 1 entries (pending siblings of its ancestors) and holds depth-of-tree slots. (The
+      // round-3 branch-free form also read the top speculatively: 3.5 % slower,
+      // r03_ab_cbvh_branchfree_c4; this one -0.7 %, r04_ab15_c4_steps.log.)
+      *slot(sp) = first0 ? entry(r1, tn1) : entry(r0, tn0);
+      sp += (h0 && h1) ? sstep : 0u;
+      ref = any ? nref : pop();
 #ifdef RT_PROF
       ++pf_box;
 #endif
