@@ -649,6 +649,14 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
   opts.push_back("-mllvm");
   opts.push_back("-disable-machine-licm");
 #endif
+#ifndef RT_JIT_SLP
+  // No SLP vectorisation: it packed the quad test's four accept compares (and the walks' hit
+  // flags) into 16-bit lane vectors (v_cndmask 0/1, shifts, v_bitop3, a compare) instead of
+  // combining them as lane masks; nothing in these kernels profits from it (the packed f32 box
+  // arithmetic is written with vector types). C4 -1.3 %, C3 -0.4 %, C2 +-0, images identical
+  // (profiles/r04_ab17_cN.log).
+  opts.push_back("-fno-slp-vectorize");
+#endif
   // build knobs of this library (ablation / occupancy variants, Makefile) apply to its
   // run-time kernels too
 #define RTJ_STR2(x) #x
