@@ -33,9 +33,20 @@ $(BUILD)/rt_jit_sources.inc: $(JIT_HDR) $(CSRC)/embed_sources.py
 	@mkdir -p $(BUILD)
 	python3 $(CSRC)/embed_sources.py $@ $(JIT_HDR)
 
-$(BUILD)/librtmi355x.so: $(DEV_SRC) $(DEV_HDR)
+# one object per source, so an edit of the host-side generator or flattener does not recompile
+# the kernels (rt_device.hip: every ahead-of-time template instance, ~3 minutes)
+OBJ      := $(BUILD)/obj
+DEV_OBJ  := $(OBJ)/rt_device.o $(OBJ)/rt_flatten.o $(OBJ)/rt_obvh.o $(OBJ)/rt_jit.o
+$(OBJ)/rt_device.o: $(CSRC)/rt_device.hip $(DEV_HDR)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(OBJ)/%.o: $(CSRC)/%.cpp $(DEV_HDR)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/librtmi355x.so: $(DEV_OBJ)
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -shared $(DEV_SRC) -o $@ -lhiprtc
+	$(HIPCC) $(HIPFLAGS) -shared $(DEV_OBJ) -o $@ -lhiprtc
 
 $(BUILD)/librtgather.so: $(CSRC)/rt_gather.hip include/rt_gather.h include/rt_mi355x.h
 	@mkdir -p $(BUILD)

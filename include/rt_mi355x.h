@@ -212,6 +212,19 @@ int rt_scene_validate(const rt_scene_blob* blob);
 #define RT_LAYOUT_STATS 11
 int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n);
 
+/* Host-only check of a product render's LDS plan and of the compact BVHs its walk reads from LDS
+ * (no device needed): out[0..17] = workgroup size, static LDS bound, staged table
+ * bytes, compact-tree LDS offset (0xffffffff: not in LDS), compact-tree bytes, stack LDS offset,
+ * stack bytes per lane (header cbvh_stack), dynamic LDS, static + dynamic, the CU's LDS, compact
+ * trees, deepest tree (internal nodes, root = 1), structural errors, largest stack slot the
+ * walk stores to, largest number of pending entries, rays walked, box steps, one past the
+ * largest compact-region byte read. The walks are a host restatement of the LDS walk over
+ * n_rays random rays per tree without closest-hit culling (the worst case for the stack).
+ * msg (may be NULL) receives the first structural error. `flags`: the render's RT_FLAG_*. */
+#define RT_LDS_CHECK 18
+int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_rays, uint64_t seed,
+                       uint64_t* out, int n, char* msg, uint32_t msg_len);
+
 /* Validate, flatten (threaded node array, f64 payloads; rt_layout.h) and upload to `device`. */
 int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* scene);
@@ -234,8 +247,11 @@ int rt_jit_check(const rt_scene_blob* blob, const char* arch, int* state, char* 
  * renders of ONE scene may be issued from several host threads and on several streams at once,
  * each into its own output buffer. Every render call takes a private slot of per-render state
  * (pool-queue word, op counters, f64 workspace, events): a slot whose previous render has
- * finished or went to the same stream, else a new one (up to 8 per scene; beyond that a call
- * waits for a slot to finish). Renders on different streams therefore run concurrently and each
+ * finished or went to the same stream handle, else a new one (up to 8 per scene; beyond that a
+ * call waits for a slot to finish); the call's stream always waits for the slot's previous
+ * render (an event wait: equal handles such as hipStreamPerThread are different streams in
+ * different threads), and a call that fails after enqueuing work still marks the slot busy
+ * until that work ends. Renders on different streams therefore run concurrently and each
  * gives its serial image bit for bit. Two renders into the SAME output buffer are ordered only by
  * the caller (same stream, or events). rt_scene_destroy must not race with renders of the scene. */
 

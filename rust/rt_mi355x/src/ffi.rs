@@ -50,6 +50,7 @@ pub const RT_FLAG_INTERPRETER: u32 = 0x8;
 pub const RT_FLAG_REFERENCE_BVH: u32 = 0x10;
 
 pub const RT_LAYOUT_STATS: c_int = 11;
+pub const RT_LDS_CHECK: c_int = 18;
 pub const RT_TRACE_HISTORY: c_int = 64;
 
 #[repr(C)]
@@ -132,6 +133,8 @@ extern "C" {
     pub fn rt_device_count(count: *mut c_int) -> c_int;
     pub fn rt_scene_validate(blob: *const rt_scene_blob) -> c_int;
     pub fn rt_scene_layout_stats(blob: *const rt_scene_blob, out: *mut u32, n: c_int) -> c_int;
+    pub fn rt_scene_lds_check(blob: *const rt_scene_blob, flags: u32, n_rays: u32, seed: u64,
+                              out: *mut u64, n: c_int, msg: *mut c_char, msg_len: u32) -> c_int;
     pub fn rt_scene_create(blob: *const rt_scene_blob, device: c_int, out: *mut *mut rt_scene)
         -> c_int;
     pub fn rt_scene_destroy(scene: *mut rt_scene);

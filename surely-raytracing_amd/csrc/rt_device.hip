@@ -208,6 +208,93 @@ int set_err(int code, const std::string& m) {
       return set_err(RT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
   } while (0)
 
+// The path kernel's LDS for one render (rt_trace's prologue stages these regions, in this order,
+// from byte 0 of the dynamic LDS): the small tables or the Perlin tables (stage), then either the
+// compact ordered BVHs and the LDS walk's per-lane stacks (cbvh_walk_t: lane l's slot k at
+// stack_off + 4 (l + k block), header cbvh_stack = 4 x the deepest tree's depth bytes per lane),
+// or as much of the reference BVH region as fits. One function for the render and for the host
+// check of the plan (rt_scene_lds_check), so the two cannot drift apart.
+struct LdsPlan {
+  int block = 0;
+  size_t static_lds = 0;  // the kernel's static LDS (per-lane f64 sums, ...), an upper bound
+  uint32_t stage_scene = 0, stage_bytes = 0, n_perlin_lds = 0;
+  uint32_t cbvh_lds_off = ~0u, stack_lds_off = 0, cbvh_bytes = 0;
+  size_t cbvh_lds = 0;  // bytes of the trees and stacks
+  uint32_t bvh_lds_words = 0, bvh_lds_off = 0;
+  size_t lds_bytes = 0;  // dynamic LDS of the launch
+};
+LdsPlan plan_lds(const rtl_scene_header& hdr, uint32_t o_perl, uint32_t flags, bool want_jit,
+                 size_t lds_module_max) {
+  LdsPlan L;
+  const bool count = (flags & RT_FLAG_COUNT_OPS) != 0;
+  const bool bvh = hdr.has_bvh != 0;
+  L.block = bvh ? kBlockBvh : kBlock;
+  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc; non-BVH
+  // kernels also the row totals sh_row and the bounce's throughput factor and ending radiance,
+  // sh_f / sh_le), the op counters, slack for the profiling build
+  L.static_lds = (size_t)L.block * (bvh ? 24 : 96) + 512 + (count ? 128 : 0);
+  // a scene whose tables up to the Perlin block fit kStageScene bytes is copied whole (per-lane
+  // reads then never leave the CU); otherwise only its first Perlin tables
+  const uint32_t used_perlins = hdr.has_textures ? hdr.n_perlins : 0u;
+  const size_t scene_prefix = o_perl + (size_t)used_perlins * RTL_PERLIN_BYTES;
+  L.stage_scene = scene_prefix <= kStageScene ? 1u : 0u;
+  if (L.stage_scene) {
+    L.n_perlin_lds = used_perlins;
+    L.stage_bytes = (uint32_t)((scene_prefix + 15) & ~(size_t)15);
+  } else {
+    L.n_perlin_lds = std::min<uint32_t>(used_perlins, kPerlinLds);
+    L.stage_bytes = L.n_perlin_lds * RTL_PERLIN_BYTES;
+  }
+  const size_t cap = (want_jit ? lds_module_max : kLdsTotal) - L.static_lds;
+  L.cbvh_bytes = hdr.cbvh_words * 4u;
+  const size_t need = (size_t)L.stage_bytes + L.cbvh_bytes + (size_t)hdr.cbvh_stack * L.block;
+  if (bvh && !count && L.cbvh_bytes && !(flags & RT_FLAG_REFERENCE_BVH) &&
+      !std::getenv("RT_NO_CBVH_LDS") && need <= cap) {
+    L.cbvh_lds_off = L.stage_bytes;
+    L.stack_lds_off = L.stage_bytes + L.cbvh_bytes;
+    L.cbvh_lds = need - L.stage_bytes;
+  }
+  if (L.stage_scene) {
+    L.bvh_lds_words = hdr.bvh_words;
+  } else if (bvh && L.cbvh_lds_off == ~0u) {
+    const size_t room = cap > L.stage_bytes ? cap - L.stage_bytes : 0;
+    L.bvh_lds_words = (uint32_t)std::min<size_t>(hdr.bvh_words, room / 64 * 16);
+    L.bvh_lds_off = L.stage_bytes;
+  }
+  L.lds_bytes = L.stage_bytes + (L.stage_scene ? 0u : (size_t)L.bvh_lds_words * 4u) + L.cbvh_lds;
+  return L;
+}
+
+// Byte offsets of the scene's tables in its one device allocation (rt_scene_create): nodes,
+// materials, textures, lights, light offsets, Perlin tables, 16-byte aligned; texels last.
+struct TableLayout {
+  size_t o_nodes = 0, o_mats = 0, o_texs = 0, o_lig = 0, o_loff = 0, o_perl = 0, o_tx = 0, total = 0;
+};
+// Bytes of TraceParams::pool for `waves` resident waves of a walker with `nt` pooled trees.
+size_t pool_bytes(int nt, size_t waves) {
+  switch (nt) {
+    case 2: return waves * PoolLayout<2>::doubles * sizeof(double);
+    case 3: return waves * PoolLayout<3>::doubles * sizeof(double);
+    case 4: return waves * PoolLayout<4>::doubles * sizeof(double);
+    default: return 0;
+  }
+}
+
+TableLayout table_layout(const rtf::FlatScene& F) {
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  TableLayout T;
+  // +256 B: the LANE walker fetches 64 bytes of every node it visits (END, 16 B, included) and
+  // prefetches one quad record past a batch
+  T.o_mats = al(T.o_nodes + F.nodes.size() * 4 + 256);
+  T.o_texs = al(T.o_mats + F.mats.size() * 4);
+  T.o_lig = al(T.o_texs + F.texs.size() * 4);
+  T.o_loff = al(T.o_lig + F.lights.size() * 4);
+  T.o_perl = al(T.o_loff + F.light_offs.size() * 4);
+  T.o_tx = al(T.o_perl + F.perlin.size());
+  T.total = al(T.o_tx + F.texels.size()) + 256;
+  return T;
+}
+
 }  // namespace
 
 // The per-render state of a scene: the f64 workspace, the pool-queue word and op counters, the
@@ -218,6 +305,8 @@ int set_err(int code, const std::string& m) {
 struct RenderSlot {
   uint8_t* work = nullptr;  // row totals / segment partials / tail samples + f64 running sums
   size_t work_bytes = 0;
+  double* pool = nullptr;   // pooled BVH walks' exchange (rt_kernel.h cbvh_pool)
+  size_t pool_bytes = 0;
   unsigned long long* ops = nullptr;  // 32 op counters, the pool-queue word (32), profiling (40..)
   unsigned int* queue = nullptr;
   hipEvent_t done = nullptr;  // recorded after the render's last kernel
@@ -251,6 +340,7 @@ struct rt_scene {
   // generated (jit_msg says why), -2 = compile failed (jit_msg = log; the interpreter runs)
   std::string jit_walker, jit_msg;
   int jit_state = -1;
+  int pool_trees = 0;  // BVH subtrees the generated walker walks as one pool (rt_jit.hpp generate)
   rtj::Kernel jit_k[4];  // [tex][staged]
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -308,6 +398,29 @@ int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n) {
   return RT_OK;
 }
 
+int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_rays, uint64_t seed,
+                       uint64_t* out, int n, char* msg, uint32_t msg_len) {
+  if (!out || n < 0) return set_err(RT_ERR_INVALID_ARG, "null out");
+  rtf::FlatScene F;
+  std::string err;
+  const int rc = rtf::flatten(blob, &F, &err);
+  if (rc != RT_OK) return set_err(rc, err);
+  const TableLayout TL = table_layout(F);
+  // the product kernel's plan on a device whose workgroups may take the CU's whole LDS
+  const LdsPlan L = plan_lds(F.hdr, (uint32_t)TL.o_perl, flags, true, kLdsTotal);
+  const rtf::WalkCheck W = rtf::check_compact_trees(F.nodes, F.hdr, n_rays, seed);
+  const uint64_t v[RT_LDS_CHECK] = {
+      (uint64_t)L.block, L.static_lds, L.stage_bytes, L.cbvh_lds_off, L.cbvh_bytes, L.stack_lds_off,
+      F.hdr.cbvh_stack, L.lds_bytes, L.static_lds + L.lds_bytes, kLdsTotal, W.trees, W.max_depth,
+      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read};
+  for (int k = 0; k < n && k < RT_LDS_CHECK; ++k) out[k] = v[k];
+  if (msg && msg_len) {
+    std::strncpy(msg, W.first_error.c_str(), msg_len - 1);
+    msg[msg_len - 1] = '\0';
+  }
+  return RT_OK;
+}
+
 int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   if (!out) return set_err(RT_ERR_INVALID_ARG, "null out");
   *out = nullptr;
@@ -315,6 +428,14 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   std::string err;
   int rc = rtf::flatten(blob, &F, &err);
   if (rc != RT_OK) return set_err(rc, err);
+  {
+    // The LDS walk (rt_kernel.h cbvh_walk_t) trusts the compact trees: its only global loads are
+    // the leaf records it reaches through their references, and its stack stores are bounded by
+    // the header's cbvh_stack. Every tree is checked before upload (structure, references, leaf
+    // records, depth; no ray walks): a malformed tree is refused here, not met on the device.
+    const rtf::WalkCheck W = rtf::check_compact_trees(F.nodes, F.hdr, 0, 0);
+    if (W.errors) return set_err(RT_ERR_BAD_BLOB, "compact BVH check: " + W.first_error);
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return set_err(RT_ERR_NO_DEVICE, "no HIP device available");
@@ -323,17 +444,15 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   // Pack the tables into one allocation, in the order the kernel stages them into LDS (a
   // prefix of it: nodes, materials, textures, lights, light offsets, Perlin tables), 16-byte
   // aligned; texels last (never staged).
-  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  size_t o_nodes = 0, s_nodes = F.nodes.size() * 4;
-  // +256 B: the LANE walker fetches 64 bytes of every node it visits (END, 16 B, included) and
-  // prefetches one quad record past a batch
-  size_t o_mats = al(o_nodes + s_nodes + 256), s_mats = F.mats.size() * 4;
-  size_t o_texs = al(o_mats + s_mats), s_texs = F.texs.size() * 4;
-  size_t o_lig = al(o_texs + s_texs), s_lig = F.lights.size() * 4;
-  size_t o_loff = al(o_lig + s_lig), s_loff = F.light_offs.size() * 4;
-  size_t o_perl = al(o_loff + s_loff), s_perl = F.perlin.size();
-  size_t o_tx = al(o_perl + s_perl), s_tx = F.texels.size();
-  size_t total = al(o_tx + s_tx) + 256;
+  const TableLayout TL = table_layout(F);
+  const size_t o_nodes = TL.o_nodes, s_nodes = F.nodes.size() * 4;
+  const size_t o_mats = TL.o_mats, s_mats = F.mats.size() * 4;
+  const size_t o_texs = TL.o_texs, s_texs = F.texs.size() * 4;
+  const size_t o_lig = TL.o_lig, s_lig = F.lights.size() * 4;
+  const size_t o_loff = TL.o_loff, s_loff = F.light_offs.size() * 4;
+  const size_t o_perl = TL.o_perl, s_perl = F.perlin.size();
+  const size_t o_tx = TL.o_tx, s_tx = F.texels.size();
+  const size_t total = TL.total;
   std::vector<uint8_t> host(total, 0);
   auto cp = [&](size_t off, const void* src, size_t n) {
     if (n) std::memcpy(host.data() + off, src, n);
@@ -386,7 +505,7 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   if (jit_env && std::strcmp(jit_env, "0") == 0) {
     sc->jit_msg = "disabled by RT_JIT=0";
   } else {
-    sc->jit_walker = rtj::generate(F, &sc->jit_msg);
+    sc->jit_walker = rtj::generate(F, &sc->jit_msg, &sc->pool_trees);
     sc->jit_state = sc->jit_walker.empty() ? -1 : 0;
   }
   sc->sphere_light0 = -1;
@@ -412,6 +531,7 @@ void rt_scene_destroy(rt_scene* sc) {
   if (sc->dev) (void)hipFree(sc->dev);
   for (const auto& sl : sc->slots) {
     if (sl->work) (void)hipFree(sl->work);
+    if (sl->pool) (void)hipFree(sl->pool);
     if (sl->ops) (void)hipFree(sl->ops);
     if (sl->done) (void)hipEventDestroy(sl->done);
     if (sl->ev0) (void)hipEventDestroy(sl->ev0);
@@ -465,7 +585,10 @@ int rt_scene_jit_info(rt_scene* sc, int* state, char* msg, uint32_t msg_len) {
 }
 
 // A slot for a render on `stream` (RenderSlot), with sc->mu held through `lock`: a free one (its
-// last render has finished, or went to the same stream), else a new one, else wait for a release.
+// last render has finished, or went to the same stream handle), else a new one, else wait for a
+// release. A reused slot's `done` event is always waited for on `stream` (hipStreamWaitEvent):
+// equal handles are not the same stream everywhere (hipStreamPerThread, the per-thread default
+// stream), so stream order alone cannot be trusted; on the same stream the wait costs nothing.
 static int acquire_slot(rt_scene* sc, std::unique_lock<std::mutex>& lock, hipStream_t stream,
                         RenderSlot** out) {
   for (;;) {
@@ -512,6 +635,7 @@ static int acquire_slot(rt_scene* sc, std::unique_lock<std::mutex>& lock, hipStr
         continue;
       }
     }
+    if (pick->recorded) HIP_TRY(hipStreamWaitEvent(stream, pick->done, 0));
     pick->held = true;
     sc->last_slot = (int)(std::find_if(sc->slots.begin(), sc->slots.end(),
                                        [&](const std::unique_ptr<RenderSlot>& u) {
@@ -522,14 +646,28 @@ static int acquire_slot(rt_scene* sc, std::unique_lock<std::mutex>& lock, hipStr
   }
 }
 
-// Releases a held slot on every exit path of a render call.
+// Releases a held slot on every exit path of a render call. Once the call has enqueued work on
+// `stream` (enqueued), a call that fails half way still records the slot's `done` event after
+// that work: the next render to take the slot then waits for the kernels that may still use its
+// workspace and queue word, instead of for the previous render's event.
 struct SlotHold {
   rt_scene* sc;
   std::unique_lock<std::mutex>& lock;
   RenderSlot* sl = nullptr;
+  hipStream_t stream = nullptr;
+  bool enqueued = false;   // work of this call is on `stream`
+  bool finished = false;   // `done` was recorded after all of it
   ~SlotHold() {
     if (!sl) return;
     if (!lock.owns_lock()) lock.lock();
+    if (enqueued && !finished) {
+      if (hipEventRecord(sl->done, stream) == hipSuccess) {
+        sl->recorded = true;
+        sl->last_stream = stream;
+      } else {
+        (void)hipStreamSynchronize(stream);  // no event: drain the stream before the slot is reused
+      }
+    }
     sl->held = false;
     sc->slot_cv.notify_all();
   }
@@ -601,70 +739,33 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   const bool vol = (sc->hdr.has_volume | sc->hdr.has_isotropic) != 0;
   const bool tex = sc->hdr.has_textures != 0;
   const bool bvh = sc->hdr.has_bvh != 0;
-  const int block = bvh ? kBlockBvh : kBlock;
-  // static LDS of the path kernel: the per-lane f64 running sums (trace_body sh_acc; non-BVH
-  // kernels also the row totals sh_row and the bounce's throughput factor and ending radiance,
-  // sh_f / sh_le), the op counters, slack for the profiling build; the dynamic LDS holds the
-  // staged tables
-  const size_t static_lds = (size_t)block * (bvh ? 24 : 96) + 512 + (count ? 128 : 0);
-  // LDS staging: a scene whose tables up to the Perlin block fit kStageScene bytes is copied
-  // whole (per-lane reads then never leave the CU); otherwise only its first Perlin tables.
-  const uint32_t used_perlins = sc->hdr.has_textures ? sc->hdr.n_perlins : 0u;
-  const size_t scene_prefix = sc->o_perl + (size_t)used_perlins * RTL_PERLIN_BYTES;
-  P.stage_scene = scene_prefix <= kStageScene ? 1u : 0u;
-  if (P.stage_scene) {
-    P.n_perlin_lds = used_perlins;
-    P.stage_src = sc->dev;
-    P.stage_bytes = (uint32_t)((scene_prefix + 15) & ~(size_t)15);
-  } else {
-    P.n_perlin_lds = std::min<uint32_t>(used_perlins, kPerlinLds);
-    P.stage_src = sc->perlin;
-    P.stage_bytes = P.n_perlin_lds * RTL_PERLIN_BYTES;
-  }
   // product renders of a generated scene run its scene-specialised kernel (same template
   // arguments and launch bounds as the ahead-of-time kernel, top-level walk unrolled; rt_jit.cpp)
   const bool want_jit = !count && !(opts->flags & RT_FLAG_INTERPRETER) && sc->jit_state >= 0;
-  // BVH region (rt_layout.h): in LDS with the small scene, else staged after the Perlin tables
-  // as far as the workgroup's LDS budget allows (the rest is read through the caches)
+  // LDS: staged tables, then the compact ordered BVHs (rt_layout.h CBVH) with the walk's
+  // per-lane stacks, or as much of the reference BVH region as fits (plan_lds); with the compact
+  // trees in LDS the reference BVH region stays in global memory (only lanes flagged for the
+  // reference-order re-walk read it)
+  const LdsPlan LP = plan_lds(sc->hdr, sc->o_perl, opts->flags, want_jit, sc->lds_module_max);
+  const int block = LP.block;
+  const size_t static_lds = LP.static_lds;
+  P.stage_scene = LP.stage_scene;
+  P.n_perlin_lds = LP.n_perlin_lds;
+  P.stage_src = LP.stage_scene ? sc->dev : sc->perlin;
+  P.stage_bytes = LP.stage_bytes;
   P.bvh_words = sc->hdr.bvh_words;
-  // Compact ordered BVHs (rt_layout.h CBVH) of a product render go to LDS after the staged
-  // tables, with the walk's per-lane stacks (cbvh_walk: one u32 per tree level, header
-  // cbvh_stack bytes); the reference BVH region then stays
-  // in global memory (only lanes flagged for the reference-order re-walk read it)
   P.cbvh_src = (const uint8_t*)(sc->nodes + sc->hdr.cbvh_word0);
-  P.cbvh_bytes = sc->hdr.cbvh_words * 4u;
-  P.cbvh_lds_off = ~0u;
-  P.stack_lds_off = 0;
-  size_t cbvh_lds = 0;
-  {
-    const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
-    const size_t need = (size_t)P.stage_bytes + P.cbvh_bytes + (size_t)sc->hdr.cbvh_stack * block;
-    if (bvh && !count && P.cbvh_bytes && !(opts->flags & RT_FLAG_REFERENCE_BVH) &&
-        !std::getenv("RT_NO_CBVH_LDS") && need <= cap) {
-      P.cbvh_lds_off = P.stage_bytes;
-      P.stack_lds_off = P.stage_bytes + P.cbvh_bytes;
-      cbvh_lds = need - P.stage_bytes;
-    }
-  }
-  if (P.stage_scene) {
-    P.bvh_lds_words = P.bvh_words;
-    P.bvh_lds_off = 0;
-  } else if (bvh && P.cbvh_lds_off != ~0u) {
-    P.bvh_lds_words = 0;
-    P.bvh_lds_off = 0;
-  } else if (bvh) {
-    const size_t cap = (want_jit ? sc->lds_module_max : kLdsTotal) - static_lds;
-    const size_t room = cap > P.stage_bytes ? cap - P.stage_bytes : 0;
-    P.bvh_lds_words = (uint32_t)std::min<size_t>(P.bvh_words, room / 64 * 16);
-    P.bvh_lds_off = P.stage_bytes;
-  }
+  P.cbvh_bytes = LP.cbvh_bytes;
+  P.cbvh_lds_off = LP.cbvh_lds_off;
+  P.stack_lds_off = LP.stack_lds_off;
+  P.bvh_lds_words = LP.bvh_lds_words;
+  P.bvh_lds_off = LP.bvh_lds_off;
   P.o_mats = sc->o_mats;
   P.o_texs = sc->o_texs;
   P.o_lights = sc->o_lights;
   P.o_loffs = sc->o_loffs;
   P.o_perl = sc->o_perl;
-  const size_t lds_bytes =
-      P.stage_bytes + (P.stage_scene ? 0u : (size_t)P.bvh_lds_words * 4u) + cbvh_lds;
+  const size_t lds_bytes = LP.lds_bytes;
   for (int k = 0; k < 3; ++k) {
     P.center[k] = cam->center[k];
     P.p00[k] = cam->pixel00_loc[k];
@@ -863,6 +964,23 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   }
   double* tot = (double*)sl->work;
   P.part = (double*)(sl->work + tot_bytes);
+  // the pooled BVH walks' exchange blocks, one per resident wave (only a scene-specialised kernel
+  // with pooled walks and the compact trees in LDS uses them)
+  P.pool = nullptr;
+  if (jfn && sc->pool_trees >= 2 && P.cbvh_lds_off != ~0u) {
+    const size_t pb = pool_bytes(sc->pool_trees, (size_t)max_blocks * (block / 64));
+    if (pb > sl->pool_bytes) {
+      if (sl->recorded) HIP_TRY(hipEventSynchronize(sl->done));
+      if (sl->pool) HIP_TRY(hipFree(sl->pool));
+      sl->pool = nullptr;
+      sl->pool_bytes = 0;
+      HIP_TRY(hipMalloc(&sl->pool, pb));
+      sl->pool_bytes = pb;
+    }
+    P.pool = sl->pool;
+  }
+  hold.stream = stream;
+  hold.enqueued = true;  // from here on a failure still records `done` (SlotHold)
   if (ops_buf) HIP_TRY(hipMemsetAsync(sl->ops, 0, sizeof(unsigned long long) * 32, stream));
 #ifdef RT_PROF
   HIP_TRY(hipMemsetAsync(sl->ops + 40, 0, sizeof(unsigned long long) * 21, stream));
@@ -908,6 +1026,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   HIP_TRY(hipEventRecord(sl->done, stream));
   sl->recorded = true;
   sl->last_stream = stream;
+  hold.finished = true;
   if (stats) {
     lock.unlock();  // the slot stays held: other renders of the scene go on meanwhile
     HIP_TRY(hipStreamSynchronize(stream));
@@ -1244,7 +1363,10 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, const rt_render_opts* opt
   hipError_t e = hipSetDevice(d0);
   if (e == hipSuccess && m->frame_recorded) e = hipStreamWaitEvent(out_stream, m->frame_done, 0);
   if (e == hipSuccess && m->stage_bytes < frame_bytes) {
+    // the previous frame's gather reads the staging buffer: it must have finished (a failed
+    // wait leaves the buffer in use, so it is reported, not freed)
     if (m->frame_recorded) e = hipEventSynchronize(m->frame_done);
+    if (e != hipSuccess) return fail(e, "staging buffer (waiting for the previous frame)");
     if (m->stage) (void)hipFree(m->stage);
     m->stage = nullptr;
     m->stage_bytes = 0;

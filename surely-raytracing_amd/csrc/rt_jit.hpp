@@ -15,7 +15,11 @@ namespace rtj {
 // time, unrolled, with every record's constants as literals; a BVH subtree record becomes a call
 // of the interpreter's per-lane walker. Empty when the scene has records the generator does not
 // emit or is too large; *why says which.
-std::string generate(const rtf::FlatScene& F, std::string* why);
+// When the top level holds 2 to 4 BVH subtrees with compact ordered BVHs, their walks run as one
+// queue per wave (rt_kernel.h cbvh_pool) and *pool_trees (may be NULL) receives their number (0:
+// no pooled walks; RT_NO_POOL=1 at scene creation turns them off for A/B). The render then
+// provides TraceParams::pool (rt_device.hip, rt_kernel.h PoolLayout).
+std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees = nullptr);
 
 // Template arguments of the path kernel (rt_kernel.h trace_body) the generated walker runs in;
 // the same as the ahead-of-time interpreter kernel the scene would otherwise launch.
@@ -45,8 +49,9 @@ void release_kernel(const Kernel& k);
 
 // The hiprtc translation unit (embedded headers + walker + rt_trace_jit wrapper) and its
 // compilation for `arch` (e.g. "gfx950") into a code object; host-only, no device needed.
+// use_cache = false bypasses the code-object cache (a cached entry that failed to load).
 std::string kernel_source(const std::string& walker, const Flags& f);
 int compile(const std::string& src, const std::string& arch, std::vector<char>* code,
-            std::string* log);
+            std::string* log, bool use_cache = true);
 
 }  // namespace rtj

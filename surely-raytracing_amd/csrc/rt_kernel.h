@@ -319,6 +319,8 @@ struct TraceParams {
   double* __restrict__ part;
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
+  // pooled BVH walks (cbvh_pool): one PoolLayout block per resident wave, or null (not pooled)
+  double* __restrict__ pool;
   int n_pools;    // pools of this launch: n_pairs_r + (pairs - n_pairs_r) * n_blk
   int n_pairs_r;  // (tile, s_j) pairs rendered as row items (one item per pixel, all s_i)
   int n_pairs_a;  // pairs [n_pairs_r, n_pairs_a): segment items; the rest one item per sample
@@ -1570,6 +1572,225 @@ __device__ __forceinline__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, 
                                                 hit_node, hit_frame, flag);
 }
 
+// ---------------------------------------------------------------- pooled BVH walks
+// A world query visits every top-level BVH subtree of the list (hittable.rs:88-109 ->
+// BvhNode::hit :216-236), and each walk runs until the wave's slowest lane is done: at C4 the
+// ground-box walk's box steps ran at a SIMD efficiency of 6.0 / 18.3 and the sphere cluster's at
+// 2.0 / 13.5. cbvh_pool walks a wave's NT x 64 trees-by-lanes as ONE queue of
+// tasks (task k: tree k >> 6 of lane k & 63): each lane starts on its own ray's first tree, and
+// lanes that finish early take the next queued task -- another lane's walk of a later tree --
+// once RT_POOL_THR lanes wait (ballot + mbcnt, one setup block for all of them), so a wave runs
+// about max(longest walk, mean work) instead of the sum of its per-tree maxima.
+//
+// Semantics. The queued walks run with tmax = +inf (the list's closest hit before each subtree
+// is not known when the pool starts), so each returns its subtree's smallest candidate t* and
+// record with cbvh_walk_t's arithmetic and tie flag. At the subtree's place in the list the
+// generated walker (rt_jit.cpp) then applies the reference's interval [tmin, closest]: t* wins
+// when t* < closest; the lane re-walks the reference tree in the reference order with the true
+// interval (traverse<LANE>, as bvh_subtree does for flagged lanes) when the walk flagged it or
+// t* lies within 3 kTieRel of closest (where the reference's answer depends on its culling and
+// visiting order: a quad at t = closest is inside Quad::hit's inclusive interval, a sphere's is
+// not, an AABB entering at closest is culled). A walk without random draws (ordered BVHs only
+// hold QUAD / QUADS / SPHERE leaves) may run at any time, so the draw order is unchanged.
+//
+// Exchange. Rays of trees 1.. and every task's result go through the wave's block of
+// TraceParams::pool (global, L2-resident: 4.3 KB per wave and tree): the owner stores its rays
+// before the pool, an executing lane reads one (7 doubles) when it takes the task and stores the
+// result (t, record | hit << 30 | flag << 31); the owner reads its NT results after the pool.
+#ifndef RT_POOL_THR
+#define RT_POOL_THR 16
+#endif
+constexpr uint32_t kPoolRay = 7;  // o.xyz, d.xyz, time (f64, one 64-lane row each)
+template <int NT>
+struct PoolLayout {  // doubles of one wave's block of TraceParams::pool
+  static constexpr uint32_t rays = (NT - 1) * kPoolRay * 64;  // trees 1.. : component rows
+  static constexpr uint32_t saved = rays;                      // the world ray (6 rows)
+  static constexpr uint32_t t = saved + 6 * 64;                // NT rows of t
+  static constexpr uint32_t code = t + NT * 64;                // NT rows of u32 codes (as doubles)
+  static constexpr uint32_t doubles = code + NT * 32;
+};
+template <int NT>
+struct PoolOut {
+  double t[NT];
+  uint32_t code[NT];  // record | hit << 30 | flag << 31
+};
+// The caller's world ray (wo, wd) is parked in the block during the walks and read back after
+// them (the same values): the path state the bounce keeps across the walks is then not held in
+// registers while the walk state is (157 -> 168 VGPRs and 19 spilled otherwise).
+template <int NT>
+__device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd)[NT],
+                                          const d3 (&o)[NT], const d3 (&d)[NT], double tm,
+                                          double tmin, PoolOut<NT>& R, d3& wo, d3& wd) {
+  static_assert(NT >= 2 && NT <= 4, "cbvh_pool: 2 to 4 trees");
+  typedef const __attribute__((address_space(3))) uint8_t* lb_t;
+  typedef __attribute__((address_space(3))) uint8_t* lbw_t;
+  typedef const __attribute__((address_space(3))) uint32_t* lw_t;
+  typedef __attribute__((address_space(3))) uint32_t* ls_t;
+  typedef const __attribute__((address_space(3))) f32x2* lf2_t;
+  typedef PoolLayout<NT> PL;
+  const gptr N = (gptr)P.nodes;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  double* const wb = P.pool + (size_t)wave * PL::doubles;
+  uint32_t* const wcode = reinterpret_cast<uint32_t*>(wb + PL::code);
+#pragma unroll
+  for (int k = 1; k < NT; ++k) {
+    double* b = wb + (k - 1) * kPoolRay * 64 + lane;
+    b[0] = o[k].x, b[64] = o[k].y, b[128] = o[k].z;
+    b[192] = d[k].x, b[256] = d[k].y, b[320] = d[k].z, b[384] = tm;
+  }
+  {
+    double* s = wb + PL::saved + lane;
+    s[0] = wo.x, s[64] = wo.y, s[128] = wo.z, s[192] = wd.x, s[256] = wd.y, s[320] = wd.z;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 4u * threadIdx.x;
+  const uint32_t sstep = 4u * blockDim.x;
+  auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
+  constexpr float kBoxPos = 1.0f + 0x1p-18f;  // tmin >= 0: cbvh_walk_t<TPOS = true>'s box test
+  const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
+  constexpr uint32_t kDone = 0xffffu;
+  // the task in flight: its ray, the ray's derived walk constants, its tree, the walk's state
+  uint32_t task = lane;
+  d3 to = o[0], td = d[0], r;
+  double ttm = tm;
+  f32x2 ix2, iy2, iz2, nox2, noy2, noz2;
+  uint32_t onx, ony, onz;
+  lb_t base;
+  lw_t refs, leaves;
+  double closest, second;
+  float close_f;
+  uint32_t hn, ref, sp;
+  bool hit;
+  auto setup = [&]() {  // cbvh_walk_t's prologue for task `task` with ray (to, td, ttm)
+    const uint32_t tr = task >> 6;
+    uint4 h = hd[0];
+#pragma unroll
+    for (int k = 1; k < NT; ++k) h = tr == (uint32_t)k ? hd[k] : h;
+    const uint32_t n_int = (h.x - 1u) >> 1;
+    base = (lb_t)rt_lds + P.cbvh_lds_off + h.y;
+    refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
+    leaves = refs + n_int;
+    const d3 inv = mk(rcp_w(td.x), rcp_w(td.y), rcp_w(td.z));
+    onx = inv.x < 0.0 ? 8u : 0u;
+    ony = inv.y < 0.0 ? 24u : 16u;
+    onz = inv.z < 0.0 ? 40u : 32u;
+    r = mk(rcp_nr1(td.x), rcp_nr1(td.y), rcp_nr1(td.z));
+    const float ox = (float)to.x, oy = (float)to.y, oz = (float)to.z;
+    const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
+    ix2 = f32x2{ix, ix}, iy2 = f32x2{iy, iy}, iz2 = f32x2{iz, iz};
+    nox2 = f32x2{-(ox * ix), -(ox * ix)}, noy2 = f32x2{-(oy * iy), -(oy * iy)},
+    noz2 = f32x2{-(oz * iz), -(oz * iz)};
+    closest = kInf;
+    second = kInf;
+    close_f = __builtin_inff();
+    hn = 0u;
+    hit = false;
+    sp = 0u;
+    ref = h.z & 0xffffu;
+  };
+  auto cand = [&](bool valid, double t, uint32_t rec) {  // cbvh_walk_t's
+    const double te = valid ? t : kInf;
+    second = fmin(second, fmax(closest, te));
+    const bool win = te < closest;
+    closest = win ? te : closest;
+    hn = win ? rec : hn;
+    hit = hit | win;
+  };
+  auto box = [&](float tnx, float tfx, float tny, float tfy, float tnz, float tfz, float& tn) {
+    tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
+    const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
+    return tn <= tf * kBoxPos;
+  };
+  auto entry = [](uint32_t child, float tn) {
+    return child | (tn < 0.0f ? 0xff800000u : (__float_as_uint(tn) & 0xffff0000u));
+  };
+  auto pop = [&]() -> uint32_t {
+    const float cut = close_f * kBoxPos;
+    while (sp > 0) {
+      sp -= sstep;
+      const uint32_t e = *slot(sp);
+      if (!(__uint_as_float(e & 0xffff0000u) > cut)) return e & 0xffffu;
+    }
+    return kDone;
+  };
+  setup();
+  bool busy = true;
+  uint32_t next = 64u;  // wave-uniform: the next unclaimed task
+  constexpr uint32_t kTasks = 64u * NT;
+  // (a guard against a pool that never drains: every iteration tests a leaf or ends a task on
+  // each lane that is not waiting, or hands out tasks, and the pool's NT x 64 tasks visit at most
+  // 2^15 leaves each (rt_layout.h CBVH), so a well-formed pool ends within NT x 2^21 iterations
+  // -- in practice a few dozen; rt_scene_create refuses malformed trees before they reach the
+  // device)
+  for (uint32_t guard = 0; guard < (uint32_t)NT << 21; ++guard) {
+    while (ref < 0x8000u) {  // cbvh_walk_t's step
+      const lb_t nb = base + ref * 48u;
+      const f32x2 NX = *reinterpret_cast<lf2_t>(nb + onx), FX = *reinterpret_cast<lf2_t>(nb + (onx ^ 8u));
+      const f32x2 NY = *reinterpret_cast<lf2_t>(nb + ony), FY = *reinterpret_cast<lf2_t>(nb + (ony ^ 8u));
+      const f32x2 NZ = *reinterpret_cast<lf2_t>(nb + onz), FZ = *reinterpret_cast<lf2_t>(nb + (onz ^ 8u));
+      const uint32_t rr = refs[ref];
+      const f32x2 tnx = __builtin_elementwise_fma(NX, ix2, nox2), tfx = __builtin_elementwise_fma(FX, ix2, nox2);
+      const f32x2 tny = __builtin_elementwise_fma(NY, iy2, noy2), tfy = __builtin_elementwise_fma(FY, iy2, noy2);
+      const f32x2 tnz = __builtin_elementwise_fma(NZ, iz2, noz2), tfz = __builtin_elementwise_fma(FZ, iz2, noz2);
+      float tn0, tn1;
+      const bool h0 = box(tnx.x, tfx.x, tny.x, tfy.x, tnz.x, tfz.x, tn0);
+      const bool h1 = box(tnx.y, tfx.y, tny.y, tfy.y, tnz.y, tfz.y, tn1);
+      const bool first0 = h0 && (!h1 || (tn0 <= tn1));
+      const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
+      const bool any = h0 || h1;
+      const uint32_t nref = first0 ? r0 : r1;
+      *slot(sp) = first0 ? entry(r1, tn1) : entry(r0, tn0);
+      sp += (h0 && h1) ? sstep : 0u;
+      ref = any ? nref : pop();
+    }
+    if (ref != kDone) {  // a leaf whose box was hit
+      const double closest_before = closest;
+      obvh_leaf(N, leaves[ref & 0x7fffu], to, td, r, ttm, tmin, cand);
+      if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
+      ref = pop();
+    }
+    if (busy && ref == kDone) {  // the task is done: its result to the owner's row
+      const bool flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
+                        (hit & (closest <= tmin * (1.0 + kTieRel)));
+      const uint32_t tr = task >> 6, ow = task & 63u;
+      wb[PL::t + tr * 64u + ow] = closest;
+      wcode[tr * 64u + ow] = hn | (hit ? 1u << 30 : 0u) | (flag ? 1u << 31 : 0u);
+      busy = false;
+    }
+    const unsigned long long idle = __ballot(!busy);
+    const unsigned long long work = __ballot(busy);
+    if (next >= kTasks) {
+      if (work == 0ull) break;
+    } else if (__popcll(idle) >= RT_POOL_THR || work == 0ull) {
+      // refill: every waiting lane takes the next queued task (rank among the waiting lanes)
+      if (!busy) {
+        const uint32_t k = next + __builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        if (k < kTasks) {
+          task = k;
+          const double* b = wb + ((k >> 6) - 1u) * kPoolRay * 64u + (k & 63u);
+          to = mk(b[0], b[64], b[128]);
+          td = mk(b[192], b[256], b[320]);
+          ttm = b[384];
+          setup();
+          busy = true;
+        }
+      }
+      next += (uint32_t)__popcll(idle);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    R.t[k] = wb[PL::t + k * 64u + lane];
+    R.code[k] = wcode[k * 64u + lane];
+  }
+  const double* s = wb + PL::saved + lane;
+  wo = mk(s[0], s[64], s[128]);
+  wd = mk(s[192], s[256], s[320]);
+}
+
 template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
@@ -1915,7 +2136,7 @@ template <int VN>
 struct TravInterpN {
   static constexpr uint32_t kScene = kScAny;
   template <bool COUNT, bool VOL, bool BVH, bool VOLB, bool VOLI>
-  static __device__ __forceinline__ bool world(const TraceParams& P, d3 ro, d3 rd, double tm,
+  static __device__ __forceinline__ bool world(const TraceParams& P, d3& ro, d3& rd, double tm,
                                                double& t, uint32_t& hn, int& hf, Rng& g,
                                                Ctr<COUNT>& C) {
     return traverse<true, COUNT, VOL, true, BVH, VOLB, VOLI, VN>(P, P.root, ~0u, ro, rd, tm, ro,

@@ -318,4 +318,233 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
   (void)rec_words;
 }
 
+namespace {
+
+uint64_t splitmix(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+double u01(uint64_t& x) { return (double)(splitmix(x) >> 11) * 0x1p-53; }
+
+// One compact tree (rt_layout.h CBVH) as the LDS walk sees it: nodes at byte 48 r, the reference
+// pairs after the n_int nodes, the leaf records after those.
+struct CTree {
+  const uint8_t* base;  // the tree's block
+  uint32_t n_int, n_leaf, root, bytes;
+  float node(uint32_t byte) const {
+    float f;
+    std::memcpy(&f, base + byte, 4);
+    return f;
+  }
+  uint32_t word(uint32_t byte) const {
+    uint32_t w;
+    std::memcpy(&w, base + byte, 4);
+    return w;
+  }
+};
+
+// The LDS walk of rt_kernel.h cbvh_walk_t for one ray with no closest hit (close_f = +inf: no
+// box is culled by a hit, no stack entry dropped), recording its stack slots and region reads.
+// TPOS: tmin >= 0 (the world walks); else the general box test of ConstantMedium boundaries.
+void emulate_walk(const CTree& T, const double o[3], const double d[3], double tmin, bool tpos,
+                  uint32_t stack_slots, WalkCheck& W, uint32_t tree_off) {
+  auto fail = [&](const char* what) {
+    if (W.errors++ == 0) W.first_error = what;
+  };
+  const double inv[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
+  const bool nx = inv[0] < 0.0, ny = inv[1] < 0.0, nz = inv[2] < 0.0;
+  const float ix = (float)inv[0], iy = (float)inv[1], iz = (float)inv[2];
+  const float ox = (float)o[0], oy = (float)o[1], oz = (float)o[2];
+  const float nox = -(ox * ix), noy = -(oy * iy), noz = -(oz * iz);
+  const float tmin_f = (float)(tmin - std::fabs(tmin) * 0x1p-20);
+  const float close_f = HUGE_VALF;
+  constexpr float kBoxRel = 0x1p-20f, kBoxPos = 1.0f + 0x1p-18f;
+  const uint32_t onx = nx ? 8u : 0u, ony = ny ? 24u : 16u, onz = nz ? 40u : 32u;
+  auto box = [&](float tnx, float tfx, float tny, float tfy, float tnz, float tfz, float& tn) {
+    tn = std::fmax(std::fmax(tmin_f, tnx), std::fmax(tny, tnz));
+    const float tf = std::fmin(std::fmin(close_f, tfx), std::fmin(tfy, tfz));
+    return tpos ? tn <= tf * kBoxPos
+                : std::fmaf(-std::fabs(tn), kBoxRel, tn) <= std::fmaf(std::fabs(tf), kBoxRel, tf);
+  };
+  auto entry = [](uint32_t child, float tn) {
+    uint32_t b;
+    std::memcpy(&b, &tn, 4);
+    return child | (tn < 0.0f ? 0xff800000u : (b & 0xffff0000u));
+  };
+  auto read = [&](uint32_t byte, uint32_t n) {
+    W.max_read = std::max<uint64_t>(W.max_read, (uint64_t)tree_off + byte + n);
+    if (byte + n > T.bytes) fail("LDS walk read past its tree's block");
+  };
+  constexpr uint32_t kDone = 0xffffu;
+  uint32_t stack[RTL_CBVH_STACK + 2];
+  uint32_t ref = T.root, sp = 0;
+  auto pop = [&]() -> uint32_t {
+    const float cut = tpos ? close_f * kBoxPos : std::fmaf(std::fabs(close_f), kBoxRel, close_f);
+    while (sp > 0) {
+      const uint32_t e = stack[--sp];
+      const uint32_t hb = e & 0xffff0000u;
+      float tb;
+      std::memcpy(&tb, &hb, 4);
+      const bool drop = tpos ? (tb > cut) : (std::fmaf(-std::fabs(tb), kBoxRel, tb) > cut);
+      if (!drop) return e & 0xffffu;
+    }
+    return kDone;
+  };
+  ++W.rays;
+  for (uint64_t guard = 0; guard < 4ull * (T.n_int + T.n_leaf) + 8; ++guard) {
+    while (ref < 0x8000u) {
+      if (ref >= T.n_int) return fail("internal reference out of range");
+      const uint32_t nb = ref * 48u;
+      read(nb, 48u);
+      read(T.n_int * 48u + 4u * ref, 4u);
+      auto pair = [&](uint32_t off, float& a, float& b) {
+        a = T.node(nb + off);
+        b = T.node(nb + off + 4u);
+      };
+      float NX0, NX1, FX0, FX1, NY0, NY1, FY0, FY1, NZ0, NZ1, FZ0, FZ1;
+      pair(onx, NX0, NX1), pair(onx ^ 8u, FX0, FX1);
+      pair(ony, NY0, NY1), pair(ony ^ 8u, FY0, FY1);
+      pair(onz, NZ0, NZ1), pair(onz ^ 8u, FZ0, FZ1);
+      const uint32_t rr = T.word(T.n_int * 48u + 4u * ref);
+      float tn0, tn1;
+      const bool h0 = box(std::fmaf(NX0, ix, nox), std::fmaf(FX0, ix, nox), std::fmaf(NY0, iy, noy),
+                          std::fmaf(FY0, iy, noy), std::fmaf(NZ0, iz, noz), std::fmaf(FZ0, iz, noz),
+                          tn0);
+      const bool h1 = box(std::fmaf(NX1, ix, nox), std::fmaf(FX1, ix, nox), std::fmaf(NY1, iy, noy),
+                          std::fmaf(FY1, iy, noy), std::fmaf(NZ1, iz, noz), std::fmaf(FZ1, iz, noz),
+                          tn1);
+      const bool first0 = h0 && (!h1 || (tn0 <= tn1));
+      const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
+      // the far child is stored to slot sp on every step (rt_kernel.h: no branch around the
+      // store) and kept only when both children are hit
+      W.max_store_slot = std::max(W.max_store_slot, sp);
+      if (sp >= stack_slots || sp > RTL_CBVH_STACK) return fail("stack store past the lane's slots");
+      stack[sp] = first0 ? entry(r1, tn1) : entry(r0, tn0);
+      if (h0 && h1) ++sp;
+      W.max_live = std::max(W.max_live, sp);
+      ++W.steps;
+      ref = (h0 || h1) ? (first0 ? r0 : r1) : pop();
+    }
+    if (ref == kDone) return;
+    if ((ref & 0x7fffu) >= T.n_leaf) return fail("leaf reference out of range");
+    read(T.n_int * 52u + 4u * (ref & 0x7fffu), 4u);
+    ref = pop();
+  }
+  fail("walk did not end");
+}
+
+}  // namespace
+
+WalkCheck check_compact_trees(const std::vector<uint32_t>& w, const rtl_scene_header& hdr,
+                              uint32_t n_rays, uint64_t seed) {
+  WalkCheck W;
+  auto fail = [&](const std::string& what) {
+    if (W.errors++ == 0) W.first_error = what;
+  };
+  if (hdr.cbvh_words == 0) return W;
+  const size_t region0 = hdr.cbvh_word0, region_bytes = (size_t)hdr.cbvh_words * 4u;
+  if (region0 % 4 != 0 || region0 + hdr.cbvh_words > w.size()) {
+    fail("CBVH region outside the node array");
+    return W;
+  }
+  const uint8_t* region = reinterpret_cast<const uint8_t*>(w.data() + region0);
+  const uint32_t stack_slots = hdr.cbvh_stack / 4u;
+  uint64_t rng = seed ^ 0x5851F42D4C957F2Dull;
+  for (size_t p = 0; p < hdr.n_rec_words; p += record_words(w[p])) {
+    if ((w[p] & 0xffu) != RTL_BVH || w[p + 3] == 0u) continue;
+    const uint32_t ob = w[p + 3];
+    if ((size_t)ob + 4 > w.size()) {
+      fail("ordered-BVH header outside the node array");
+      continue;
+    }
+    if (w[ob + 1] == 0xffffffffu) continue;  // no compact copy: walked from the global streams
+    CTree T;
+    const uint32_t n_entries = w[ob], off = w[ob + 1];
+    T.n_int = n_entries ? (n_entries - 1u) >> 1 : 0u;
+    T.n_leaf = T.n_int + 1u;
+    T.root = w[ob + 2] & 0xffffu;
+    const size_t words = T.n_int ? ((size_t)T.n_int * 13 + T.n_leaf + 3) & ~(size_t)3 : 4u;
+    T.bytes = (uint32_t)(words * 4);
+    ++W.trees;
+    if (n_entries == 0 || (n_entries & 1u) == 0u || off % 16 != 0 || off + (size_t)T.bytes > region_bytes) {
+      fail("compact tree block malformed or outside the CBVH region");
+      continue;
+    }
+    T.base = region + off;
+    // structure: every internal node and leaf reached exactly once from the root; depth
+    std::vector<uint8_t> seen_int(T.n_int, 0), seen_leaf(T.n_leaf, 0);
+    uint32_t depth = 0;
+    bool ok = true;
+    std::vector<std::pair<uint32_t, uint32_t>> todo = {{T.root, 1u}};
+    while (!todo.empty() && ok) {
+      const auto [r, dd] = todo.back();
+      todo.pop_back();
+      if (r >= 0x8000u) {
+        const uint32_t li = r & 0x7fffu;
+        if (r == 0xffffu || li >= T.n_leaf || seen_leaf[li]++) {
+          fail("leaf reference invalid or reached twice");
+          ok = false;
+          break;
+        }
+        const uint32_t rec = T.word(T.n_int * 52u + 4u * li);
+        const uint32_t ty = rec < hdr.n_rec_words ? (w[rec] & 0xffu) : 0xffu;
+        size_t end = 0;
+        if (ty == RTL_QUADS) end = (size_t)rec + 4 + (size_t)(w[rec] >> 8) * RTL_QUAD_WORDS;
+        else if (ty == RTL_QUAD) end = (size_t)rec + RTL_QUAD_WORDS;
+        else if (ty == RTL_SPHERE) end = (size_t)rec + RTL_SPHERE_WORDS;
+        if (end == 0 || end > hdr.n_rec_words) {
+          fail("leaf record is not a QUAD / QUADS / SPHERE record inside the record region");
+          ok = false;
+        }
+        continue;
+      }
+      if (r >= T.n_int || seen_int[r]++) {
+        fail("internal reference invalid or reached twice");
+        ok = false;
+        break;
+      }
+      depth = std::max(depth, dd);
+      const uint32_t rr = T.word(T.n_int * 48u + 4u * r);
+      todo.push_back({rr >> 16, dd + 1});
+      todo.push_back({rr & 0xffffu, dd + 1});
+    }
+    if (!ok) continue;
+    for (uint32_t k = 0; k < T.n_int; ++k) ok = ok && seen_int[k];
+    for (uint32_t k = 0; k < T.n_leaf; ++k) ok = ok && seen_leaf[k];
+    if (!ok) {
+      fail("a node or leaf of the block is unreachable from the root");
+      continue;
+    }
+    if (T.n_int == 0) depth = 1;  // a single leaf (rt_obvh.cpp compact_tree)
+    W.max_depth = std::max(W.max_depth, depth);
+    if (4u * depth > hdr.cbvh_stack) fail("tree deeper than the header's cbvh_stack");
+    if (T.n_int == 0) continue;
+    // the root box: both children of node 0
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(T.node(16u * a), T.node(16u * a + 4u));
+      hi[a] = std::max(T.node(16u * a + 8u), T.node(16u * a + 12u));
+    }
+    for (uint32_t k = 0; k < n_rays; ++k) {
+      double o[3], d[3];
+      for (int a = 0; a < 3; ++a) {
+        const double ext = hi[a] - lo[a];
+        o[a] = lo[a] - 0.25 * ext + 1.5 * ext * u01(rng);
+      }
+      double n2 = 0.0;
+      do {
+        n2 = 0.0;
+        for (int a = 0; a < 3; ++a) d[a] = 2.0 * u01(rng) - 1.0, n2 += d[a] * d[a];
+      } while (n2 > 1.0 || n2 < 1e-6);
+      if (k % 8 == 7) d[k / 8 % 3] = (k & 64) ? -0.0 : 0.0;  // a ray in a slab plane: 1/d = +-inf
+      const bool tpos = (k & 1) == 0;
+      emulate_walk(T, o, d, tpos ? 1e-4 : -HUGE_VAL, tpos, stack_slots, W, off);
+    }
+  }
+  if (W.max_read > region_bytes) fail("LDS walk read past the CBVH region");
+  return W;
+}
+
 }  // namespace rtf

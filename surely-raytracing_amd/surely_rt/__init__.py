@@ -203,6 +203,9 @@ def load_device_lib(path: Path) -> C.CDLL:
         "rt_multi_destroy": (None, [p]),
         "rt_jit_check": (C.c_int, [C.POINTER(RtSceneBlob), C.c_char_p, C.POINTER(C.c_int),
                                    C.c_char_p, C.c_uint32]),
+        "rt_scene_lds_check": (C.c_int, [C.POINTER(RtSceneBlob), C.c_uint32, C.c_uint32,
+                                         C.c_uint64, C.POINTER(C.c_uint64), C.c_int, C.c_char_p,
+                                         C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -497,6 +500,10 @@ def render_par_lights(blob: Blob, cam: RtCamera, seed: int = 1, device: int = 0,
 LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volumes",
                 "volumes_one_walk_sphere", "volumes_one_walk_quads", "lights", "ordered_bvhs",
                 "compact_bvhs", "compact_bvh_bytes"]
+# rt_scene_lds_check (include/rt_mi355x.h RT_LDS_CHECK)
+LDS_CHECK = ["block", "static_lds", "stage_bytes", "cbvh_lds_off", "cbvh_bytes", "stack_lds_off",
+             "cbvh_stack", "lds_bytes", "lds_total", "lds_cu", "trees", "max_depth", "errors",
+             "max_store_slot", "max_live", "rays", "steps", "max_read"]
 
 
 def render_multi(blob: "Blob", cam: RtCamera, opts: RtRenderOpts, devices,
@@ -558,6 +565,19 @@ def layout_stats(blob: "Blob") -> dict:
     out = (C.c_uint32 * len(LAYOUT_STATS))()
     _check_dev(device_lib().rt_scene_layout_stats(blob.ref(), out, len(LAYOUT_STATS)))
     return dict(zip(LAYOUT_STATS, (int(v) for v in out)))
+
+
+def lds_check(blob: "Blob", flags: int = 0, n_rays: int = 4096, seed: int = 1) -> dict:
+    """Host-only: the product render's LDS plan and a check of the compact BVHs the LDS walk
+    reads, with a host restatement of the walk's stack and region addressing over random rays
+    (rt_scene_lds_check). `first_error` is empty when every tree is well formed."""
+    out = (C.c_uint64 * len(LDS_CHECK))()
+    msg = C.create_string_buffer(512)
+    _check_dev(device_lib().rt_scene_lds_check(blob.ref(), flags, n_rays, seed, out,
+                                               len(LDS_CHECK), msg, len(msg)))
+    d = dict(zip(LDS_CHECK, (int(v) for v in out)))
+    d["first_error"] = msg.value.decode(errors="replace")
+    return d
 
 
 def jit_check(blob: "Blob", arch: str = "gfx950") -> tuple[int, str]:

@@ -431,6 +431,12 @@ def _frame_report(cfg, acc_g, acc_o, spp):
     return flips
 
 
+# Flip-pixel ceilings of the five C4 bands: 1.25 x the counts at the round-4 head (753, 778, 790,
+# 712, 746; profiles/r04y_gputest.log), so a change that makes the device drift further from the
+# oracle's paths fails here although every pixel stays within TOL.
+C4_FLIP_CEILING = {2: 941, 6: 972, 10: 987, 14: 890, 18: 932}
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("cfg,name,kw,rows,ops_rtol", [
     ("C2", "cornell_box", dict(width=800, spp=1000), (0, 1, 800), 0.0),
@@ -453,6 +459,8 @@ def test_baseline_config_frames_vs_oracle(gpu_available, cfg, name, kw, rows, op
     flips = _frame_report(cfg, acc_g, acc_o, cam.samples_per_pixel)
     if ops_rtol == 0.0:
         assert flips == 0
+    else:
+        assert flips <= C4_FLIP_CEILING[b], (cfg, flips)
 
 
 @pytest.mark.timeout(300)

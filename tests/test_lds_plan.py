@@ -1,0 +1,67 @@
+"""Host checks of the LDS walk's invariants (no GPU).
+
+The product BVH kernels stage the compact ordered BVHs (rt_layout.h CBVH) and one stack per lane
+in LDS and walk them in cbvh_walk_t (rt_kernel.h), which stores the far child to the lane's next
+stack slot on EVERY step (kept only when both children are hit). Its memory safety rests on:
+  * the tree's internal-node depth x 4 <= the header's cbvh_stack (bytes per lane), since a node
+    of depth k has at most k - 1 pending entries and its step stores to slot k - 1;
+  * stage + trees + cbvh_stack x workgroup size fitting the dynamic LDS the launch requests, with
+    the static LDS inside the CU's 160 KiB;
+  * every reference, leaf index and leaf record of a tree being in range, so that the walk's only
+    global loads (the leaf records, the BvhNode::hit restatement of hittable.rs:216-236 they feed)
+    stay inside the scene.
+rt_scene_lds_check computes the render's LDS plan with the function the render itself uses
+(plan_lds) and restates the walk's addressing on the host over random rays WITHOUT closest-hit
+culling (every box the slab test keeps is visited, the worst case for the stack)."""
+import pytest
+
+import surely_rt as rt
+
+PRESETS = ["cornell_box", "cornell_smoke", "final_scene", "quads", "simple_light", "two_spheres",
+           "two_perlin_spheres", "earth", "three_spheres", "random_balls"]
+
+
+def _assert_walk_invariants(chk, label):
+    assert chk["errors"] == 0, (label, chk["first_error"])
+    if chk["trees"] == 0:
+        return
+    # depth x 4 <= cbvh_stack, and the walk stored only to slots below the depth
+    assert 4 * chk["max_depth"] <= chk["cbvh_stack"], (label, chk)
+    assert chk["rays"] > 0 and chk["steps"] > 0, (label, chk)
+    assert chk["max_store_slot"] < chk["max_depth"], (label, chk)
+    assert chk["max_live"] <= chk["max_depth"] - 1, (label, chk)
+    assert chk["max_read"] <= chk["cbvh_bytes"], (label, chk)
+    if chk["cbvh_lds_off"] != 0xFFFFFFFF:  # trees and stacks in LDS: the regions fit the request
+        assert chk["cbvh_lds_off"] == chk["stage_bytes"]
+        assert chk["stack_lds_off"] == chk["cbvh_lds_off"] + chk["cbvh_bytes"]
+        assert chk["stack_lds_off"] + chk["cbvh_stack"] * chk["block"] == chk["lds_bytes"], (label, chk)
+        assert chk["lds_total"] <= chk["lds_cu"] == 160 * 1024, (label, chk)
+
+
+@pytest.mark.parametrize("name", PRESETS)
+def test_presets_lds_plan_and_walk(name):
+    blob, _ = rt.preset_blob(name, width=64, spp=4)
+    _assert_walk_invariants(rt.lds_check(blob, n_rays=2048), name)
+
+
+def test_final_scene_at_benchmark_size_stages_its_trees():
+    """C4 (BASELINE configs[3]): both compact trees and the 768 lanes' stacks are in LDS."""
+    blob, _ = rt.preset_blob("final_scene", width=800, spp=5000, depth=40)
+    chk = rt.lds_check(blob, n_rays=20000)
+    _assert_walk_invariants(chk, "final_scene")
+    assert chk["trees"] == 2 and chk["block"] == 768
+    assert chk["cbvh_lds_off"] != 0xFFFFFFFF
+    assert 1 <= chk["max_depth"] <= 32
+    # the op-counting build and the reference-order flag never stage the compact trees
+    for flags in (rt.RT_FLAG_COUNT_OPS, rt.RT_FLAG_REFERENCE_BVH):
+        assert rt.lds_check(blob, flags=flags, n_rays=0)["cbvh_lds_off"] == 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_dense_bvh_fuzz_scenes_lds_plan_and_walk(seed):
+    from test_bvh_fuzz_gpu import dense_bvh_scene
+
+    blob, _ = dense_bvh_scene(seed)
+    chk = rt.lds_check(blob, n_rays=4096, seed=seed)
+    assert chk["trees"] >= 2
+    _assert_walk_invariants(chk, f"fuzz{seed}")

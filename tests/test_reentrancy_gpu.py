@@ -91,3 +91,41 @@ def test_two_host_threads_render_one_scene(gpu_available, name, kw):
         for acc, n in got[s]:
             assert np.array_equal(acc, serial[s])
             assert n == cam.image_width * cam.image_height * cam.samples_per_pixel
+
+
+def test_per_thread_default_stream_from_two_threads(gpu_available):
+    """hipStreamPerThread has one handle value but is a different stream in each host thread
+    (ADVICE r4): a render must not take a slot whose previous render, issued by another thread
+    on "the same" handle, may still be running. Each thread issues four renders back to back on
+    hipStreamPerThread without synchronising, then checks its buffer."""
+    from hip_buf import DevBuf, hip
+
+    blob, cam = rt.preset_blob("cornell_box", width=400, spp=256)
+    ds = rt.DeviceScene(blob)
+    seeds = (31, 32)
+    serial = {s: ds.render(cam, rt.make_opts(cam, seed=s))[0] for s in seeds}
+    per_thread = 2  # hipStreamPerThread (hip_runtime_api.h)
+    bufs = {s: DevBuf(serial[s].shape) for s in seeds}
+    errors: list[BaseException] = []
+    got: dict[int, np.ndarray] = {}
+
+    def work(s):
+        try:
+            for _ in range(4):
+                ds.render_device(cam, rt.make_opts(cam, seed=s), bufs[s].ptr, per_thread)
+            assert hip().hipStreamSynchronize(per_thread) == 0
+            got[s] = bufs[s].download()
+        except BaseException as e:  # surfaced in the main thread
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(s,)) for s in seeds]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for b in bufs.values():
+        b.free()
+    ds.close()
+    assert not errors, errors
+    for s in seeds:
+        assert np.array_equal(got[s], serial[s])
