@@ -7,7 +7,8 @@ Workload (BASELINE configs[1]): the reference's cornell_box scen
 
 A "step" = one full frame: every rank renders its cyclic share of the 800 rows
 (row r -> rank r % N, no data-path collective) into a device buffer, then the frame is
-gathered to rank 0 (torch.distributed: RCCL over xGMI). Scene upload, RCCL init and the
+gathered to rank 0 by the product's C-ABI gather (rt_gather_frame: ncclGather over RCCL/xGMI;
+the field "gather" names it; the one-GPU gloo rehearsal uses torch.distributed.gather). Scene upload, RCCL init and the
 op-count pass are outside the timed region. value = W*H*spp_eff*steps / max-over-ranks time.
 
 Also reported (one JSON line on rank 0):
@@ -145,7 +146,8 @@ def main():
 
     import surely_rt as rt
     from surely_rt import roofline
-    from surely_rt.parallel import cyclic_rows, gather_frame, max_rows, rank_report
+    from surely_rt.parallel import (GATHER_RCCL, RcclFrameGather, cyclic_rows, gather_choice,
+                                    gather_frame, max_rows, rank_report)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -174,6 +176,24 @@ def main():
     opts = rt.make_opts(cam, seed=args.seed, row_begin=b, row_step=s, n_rows=n,
                         flags=rt.RT_FLAG_OVERWRITE, device=local)
     stream = torch.cuda.current_stream()
+    # The frame gather to rank 0 (surely_rt.parallel.gather_choice): at N > 1 with a GPU per rank
+    # the product's C-ABI gather, rt_gather_frame (one ncclGather + the de-interleave kernel on
+    # rank 0, librtgather.so); torch.distributed only carries its communicator id. The one-GPU
+    # rehearsal keeps torch.distributed.gather over gloo.
+    gather_name = gather_choice(world, rehearse)
+    # RT_BENCH_RCCL1=1: the N > 1 gather code on one GPU (a one-rank RCCL communicator in this
+    # torch process), the rehearsal of the driver's multi-GPU path that a one-GPU box allows
+    if world == 1 and os.environ.get("RT_BENCH_RCCL1") == "1":
+        gather_name = GATHER_RCCL
+    rccl = None
+    if gather_name == GATHER_RCCL:
+        uid = [RcclFrameGather.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        rccl = RcclFrameGather(uid[0], world, rank, device=local)
+        if rank == 0:
+            scratch = torch.empty((world * m, W, 3), dtype=torch.float32, device=f"cuda:{local}")
+            frame_buf = torch.empty((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
 
     def step(ev=None):
         if ev is not None:
@@ -181,7 +201,12 @@ def main():
         ds.render_device(cam, opts, local_buf.data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        out = gather_frame(local_buf.cpu() if rehearse else local_buf, H, rank, world)
+        if rccl is not None:
+            rccl.gather(local_buf.data_ptr(), W, H, scratch.data_ptr() if rank == 0 else 0,
+                        frame_buf.data_ptr() if rank == 0 else 0, stream.cuda_stream)
+            out = frame_buf if rank == 0 else None
+        else:
+            out = gather_frame(local_buf.cpu() if rehearse else local_buf, H, rank, world)
         if ev is not None:
             ev[2].record(stream)  # the gather has completed on this stream
         return out
@@ -259,6 +284,7 @@ def main():
                 "seed": args.seed, "parallelism": f"cyclic rows x{world}, gather to rank 0",
                 "walker": walker,
             },
+            "gather": gather_name,
         }
         if ranks is not None:
             res["ranks"] = ranks
@@ -334,6 +360,8 @@ def main():
         assert frame is not None and frame.shape == (H, W, 3)
         print(json.dumps(res), flush=True)
     ds.close()
+    if rccl is not None:
+        rccl.close()
     if world > 1:
         dist.destroy_process_group()
 

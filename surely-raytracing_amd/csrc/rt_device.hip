@@ -221,6 +221,7 @@ struct LdsPlan {
   uint32_t cbvh_lds_off = ~0u, stack_lds_off = 0, cbvh_bytes = 0;
   size_t cbvh_lds = 0;  // bytes of the trees and stacks
   uint32_t bvh_lds_words = 0, bvh_lds_off = 0;
+  uint32_t row_lds_off = ~0u;  // BVH kernels: the row items' row totals (~0u: no row items)
   size_t lds_bytes = 0;  // dynamic LDS of the launch
 };
 LdsPlan plan_lds(const rtl_scene_header& hdr, uint32_t o_perl, uint32_t flags, bool want_jit,
@@ -262,6 +263,15 @@ LdsPlan plan_lds(const rtl_scene_header& hdr, uint32_t o_perl, uint32_t flags, b
     L.bvh_lds_off = L.stage_bytes;
   }
   L.lds_bytes = L.stage_bytes + (L.stage_scene ? 0u : (size_t)L.bvh_lds_words * 4u) + L.cbvh_lds;
+  // BVH product kernels with the compact trees in LDS: the row items' per-lane row totals after
+  // them when they fit (C4: 124 + 18 KB dynamic, 18 KB static), so that a whole frame keeps one
+  // f64 value per (pixel, s_j) instead of one per block of kPoolSi samples
+  const size_t row_bytes = (size_t)L.block * 3 * sizeof(double);
+  if (bvh && L.cbvh_lds_off != ~0u && !std::getenv("RT_NO_BVH_ROWS") &&
+      L.lds_bytes + row_bytes <= cap) {
+    L.row_lds_off = (uint32_t)L.lds_bytes;
+    L.lds_bytes += row_bytes;
+  }
   return L;
 }
 
@@ -412,7 +422,7 @@ int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_ray
   const uint64_t v[RT_LDS_CHECK] = {
       (uint64_t)L.block, L.static_lds, L.stage_bytes, L.cbvh_lds_off, L.cbvh_bytes, L.stack_lds_off,
       F.hdr.cbvh_stack, L.lds_bytes, L.static_lds + L.lds_bytes, kLdsTotal, W.trees, W.max_depth,
-      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read};
+      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read, L.row_lds_off};
   for (int k = 0; k < n && k < RT_LDS_CHECK; ++k) out[k] = v[k];
   if (msg && msg_len) {
     std::strncpy(msg, W.first_error.c_str(), msg_len - 1);
@@ -760,6 +770,7 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   P.stack_lds_off = LP.stack_lds_off;
   P.bvh_lds_words = LP.bvh_lds_words;
   P.bvh_lds_off = LP.bvh_lds_off;
+  P.row_lds_off = LP.row_lds_off;
   P.o_mats = sc->o_mats;
   P.o_texs = sc->o_texs;
   P.o_lights = sc->o_lights;
@@ -911,11 +922,11 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   //  * Smaller launches (an N-way share, chunks) balance better without rows (C2 over 8 GPUs:
   //    0.940 of ideal with segments, 0.894 with half the pairs as rows, profiles/
   //    r03_scaling_probe_*.log): segment items, then a tail of one pair per resident wave.
-  //  * BVH kernels keep their LDS for the compact trees and render no rows.
+  //  * BVH kernels render rows when their plan fits the row totals beside the compact trees.
   // RT_SEG_PAIRS (rows with that band) and RT_TAIL_PAIRS override the sizes (tests: the image
   // does not depend on the split).
   const int64_t res_waves = max_blocks * (block / 64);
-  const bool rows_ok = !bvh;
+  const bool rows_ok = !bvh || LP.row_lds_off != ~0u;
   const char* seg_env = std::getenv("RT_SEG_PAIRS");
   const char* tail_env = std::getenv("RT_TAIL_PAIRS");
   struct Split {

@@ -430,8 +430,10 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
         x = N[x + 1];  // QUADS, VOLUME, DUP, OTHER: their skip
       }
     }
-    const char* off = std::getenv("RT_NO_POOL");
-    if (pool.size() < 2 || (off && *off && *off != '0')) pool.clear();
+    // opt-in (RT_POOL=1 at scene creation): measured slower at C4 (DESIGN.md §4.1c "Pooled
+    // walks": +14 % kernel time, lane utilisation 0.334 -> 0.379 but 28 % more lane work)
+    const char* on = std::getenv("RT_POOL");
+    if (pool.size() < 2 || !(on && *on && *on != '0')) pool.clear();
     if (pool.size() > 4) pool.resize(4);
   }
   const int NT = (int)pool.size();
@@ -924,9 +926,12 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
                std::string* log) {
   const std::string s = kernel_source(walker, f);
   std::lock_guard<std::mutex> lock(g_mu);
-  // compile() reads RT_JIT_SRC_DIR's headers when set (diagnostics): part of the module's identity
+  // compile() reads RT_JIT_SRC_DIR's headers and RT_JIT_OPTS's options when set (diagnostics):
+  // part of the module's identity, so an A/B in one process gets one module per setting
   const char* src_dirs = std::getenv("RT_JIT_SRC_DIR");
-  auto key = std::make_pair(device, src_dirs ? s + "//" + src_dirs : s);
+  const char* jit_opts = std::getenv("RT_JIT_OPTS");
+  auto key = std::make_pair(device, s + "//" + (src_dirs ? src_dirs : "") + "//" +
+                                        (jit_opts ? jit_opts : ""));
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
     ++it->second.holds;

@@ -17,7 +17,7 @@ namespace rtj {
 // emit or is too large; *why says which.
 // When the top level holds 2 to 4 BVH subtrees with compact ordered BVHs, their walks run as one
 // queue per wave (rt_kernel.h cbvh_pool) and *pool_trees (may be NULL) receives their number (0:
-// no pooled walks; RT_NO_POOL=1 at scene creation turns them off for A/B). The render then
+// no pooled walks). Opt-in, RT_POOL=1 at scene creation: slower at C4. The render then
 // provides TraceParams::pool (rt_device.hip, rt_kernel.h PoolLayout).
 std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees = nullptr);
 

@@ -345,6 +345,9 @@ struct TraceParams {
   // global memory), and the walk's per-lane u16 stacks at stack_lds_off
   const uint8_t* cbvh_src;
   uint32_t cbvh_bytes, cbvh_lds_off, stack_lds_off;
+  // BVH kernels: the row items' per-lane f64 row totals (3 x blockDim doubles) at this dynamic
+  // LDS byte offset (row pools only when the plan placed them: n_pairs_r = 0 otherwise)
+  uint32_t row_lds_off;
   uint32_t o_mats, o_texs, o_lights, o_loffs, o_perl;
   double center[3], p00[3], du[3], dv[3], ddu[3], ddv[3], bg[3];
   double rs;
@@ -1600,13 +1603,17 @@ __device__ __forceinline__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, 
 #ifndef RT_POOL_THR
 #define RT_POOL_THR 16
 #endif
-constexpr uint32_t kPoolRay = 7;  // o.xyz, d.xyz, time (f64, one 64-lane row each)
+// One queued task of trees 1..: its ray in f64 (7 rows: o.xyz, d.xyz, time) and the walk's f32
+// slab constants (7 word rows: 1/d.xyz, -o/d.xyz as f32, the octant's bound offsets packed), all
+// formed by the owner with every lane of the wave active, so that a refill only loads them.
+constexpr uint32_t kPoolRayD = 7, kPoolRayW = 7;
 template <int NT>
 struct PoolLayout {  // doubles of one wave's block of TraceParams::pool
-  static constexpr uint32_t rays = (NT - 1) * kPoolRay * 64;  // trees 1.. : component rows
-  static constexpr uint32_t saved = rays;                      // the world ray (6 rows)
-  static constexpr uint32_t t = saved + 6 * 64;                // NT rows of t
-  static constexpr uint32_t code = t + NT * 64;                // NT rows of u32 codes (as doubles)
+  static constexpr uint32_t rays = 0;                                   // (NT-1) x 7 f64 rows
+  static constexpr uint32_t cst = (NT - 1) * kPoolRayD * 64;            // (NT-1) x 7 u32 rows
+  static constexpr uint32_t saved = cst + (NT - 1) * kPoolRayW * 32;    // the world ray: 6 rows
+  static constexpr uint32_t t = saved + 6 * 64;                         // NT rows of t
+  static constexpr uint32_t code = t + NT * 64;                         // NT u32 rows of codes
   static constexpr uint32_t doubles = code + NT * 32;
 };
 template <int NT>
@@ -1632,25 +1639,44 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   double* const wb = P.pool + (size_t)wave * PL::doubles;
+  uint32_t* const wcst = reinterpret_cast<uint32_t*>(wb + PL::cst);
   uint32_t* const wcode = reinterpret_cast<uint32_t*>(wb + PL::code);
+  // a ray's walk constants (cbvh_walk_t's prologue): f32 1/d and -o/d, the octant's offsets
+  struct Cst {
+    float ix, iy, iz, nx, ny, nz;
+    uint32_t oct;  // onx | ony << 8 | onz << 16
+  };
+  auto consts = [](d3 ro_, d3 rd_) {
+    const d3 inv = mk(rcp_w(rd_.x), rcp_w(rd_.y), rcp_w(rd_.z));
+    Cst c;
+    c.ix = (float)inv.x, c.iy = (float)inv.y, c.iz = (float)inv.z;
+    c.nx = -((float)ro_.x * c.ix), c.ny = -((float)ro_.y * c.iy), c.nz = -((float)ro_.z * c.iz);
+    c.oct = (inv.x < 0.0 ? 8u : 0u) | (inv.y < 0.0 ? 24u : 16u) << 8 | (inv.z < 0.0 ? 40u : 32u) << 16;
+    return c;
+  };
 #pragma unroll
-  for (int k = 1; k < NT; ++k) {
-    double* b = wb + (k - 1) * kPoolRay * 64 + lane;
+  for (int k = 1; k < NT; ++k) {  // the owner publishes its tasks of trees 1..
+    double* b = wb + PL::rays + (k - 1) * kPoolRayD * 64 + lane;
     b[0] = o[k].x, b[64] = o[k].y, b[128] = o[k].z;
     b[192] = d[k].x, b[256] = d[k].y, b[320] = d[k].z, b[384] = tm;
+    const Cst c = consts(o[k], d[k]);
+    uint32_t* w = wcst + (k - 1) * kPoolRayW * 64 + lane;
+    w[0] = __float_as_uint(c.ix), w[64] = __float_as_uint(c.iy), w[128] = __float_as_uint(c.iz);
+    w[192] = __float_as_uint(c.nx), w[256] = __float_as_uint(c.ny), w[320] = __float_as_uint(c.nz);
+    w[384] = c.oct;
   }
   {
-    double* s = wb + PL::saved + lane;
-    s[0] = wo.x, s[64] = wo.y, s[128] = wo.z, s[192] = wd.x, s[256] = wd.y, s[320] = wd.z;
+    double* sv = wb + PL::saved + lane;
+    sv[0] = wo.x, sv[64] = wo.y, sv[128] = wo.z, sv[192] = wd.x, sv[256] = wd.y, sv[320] = wd.z;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 4u * threadIdx.x;
   const uint32_t sstep = 4u * blockDim.x;
   auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
   constexpr float kBoxPos = 1.0f + 0x1p-18f;  // tmin >= 0: cbvh_walk_t<TPOS = true>'s box test
   const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
   constexpr uint32_t kDone = 0xffffu;
-  // the task in flight: its ray, the ray's derived walk constants, its tree, the walk's state
+  // the task in flight (or, on a waiting lane, the last one finished): its ray, walk constants,
+  // tree and walk state
   uint32_t task = lane;
   d3 to = o[0], td = d[0], r;
   double ttm = tm;
@@ -1662,7 +1688,7 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
   float close_f;
   uint32_t hn, ref, sp;
   bool hit;
-  auto setup = [&]() {  // cbvh_walk_t's prologue for task `task` with ray (to, td, ttm)
+  auto start = [&](Cst c) {  // cbvh_walk_t's prologue from the task's constants
     const uint32_t tr = task >> 6;
     uint4 h = hd[0];
 #pragma unroll
@@ -1671,16 +1697,10 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
     base = (lb_t)rt_lds + P.cbvh_lds_off + h.y;
     refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
     leaves = refs + n_int;
-    const d3 inv = mk(rcp_w(td.x), rcp_w(td.y), rcp_w(td.z));
-    onx = inv.x < 0.0 ? 8u : 0u;
-    ony = inv.y < 0.0 ? 24u : 16u;
-    onz = inv.z < 0.0 ? 40u : 32u;
+    onx = c.oct & 0xffu, ony = (c.oct >> 8) & 0xffu, onz = c.oct >> 16;
     r = mk(rcp_nr1(td.x), rcp_nr1(td.y), rcp_nr1(td.z));
-    const float ox = (float)to.x, oy = (float)to.y, oz = (float)to.z;
-    const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
-    ix2 = f32x2{ix, ix}, iy2 = f32x2{iy, iy}, iz2 = f32x2{iz, iz};
-    nox2 = f32x2{-(ox * ix), -(ox * ix)}, noy2 = f32x2{-(oy * iy), -(oy * iy)},
-    noz2 = f32x2{-(oz * iz), -(oz * iz)};
+    ix2 = f32x2{c.ix, c.ix}, iy2 = f32x2{c.iy, c.iy}, iz2 = f32x2{c.iz, c.iz};
+    nox2 = f32x2{c.nx, c.nx}, noy2 = f32x2{c.ny, c.ny}, noz2 = f32x2{c.nz, c.nz};
     closest = kInf;
     second = kInf;
     close_f = __builtin_inff();
@@ -1688,6 +1708,13 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
     hit = false;
     sp = 0u;
     ref = h.z & 0xffffu;
+  };
+  auto publish = [&]() {  // the finished task's result to its owner's row
+    const bool flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
+                      (hit & (closest <= tmin * (1.0 + kTieRel)));
+    const uint32_t tr = task >> 6, ow = task & 63u;
+    wb[PL::t + tr * 64u + ow] = closest;
+    wcode[tr * 64u + ow] = hn | (hit ? 1u << 30 : 0u) | (flag ? 1u << 31 : 0u);
   };
   auto cand = [&](bool valid, double t, uint32_t rec) {  // cbvh_walk_t's
     const double te = valid ? t : kInf;
@@ -1714,7 +1741,7 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
     }
     return kDone;
   };
-  setup();
+  start(consts(to, td));
   bool busy = true;
   uint32_t next = 64u;  // wave-uniform: the next unclaimed task
   constexpr uint32_t kTasks = 64u * NT;
@@ -1750,45 +1777,49 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
       if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
       ref = pop();
     }
-    if (busy && ref == kDone) {  // the task is done: its result to the owner's row
-      const bool flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
-                        (hit & (closest <= tmin * (1.0 + kTieRel)));
-      const uint32_t tr = task >> 6, ow = task & 63u;
-      wb[PL::t + tr * 64u + ow] = closest;
-      wcode[tr * 64u + ow] = hn | (hit ? 1u << 30 : 0u) | (flag ? 1u << 31 : 0u);
-      busy = false;
-    }
+    busy = busy && ref != kDone;  // a finished task waits with its result in registers
     const unsigned long long idle = __ballot(!busy);
     const unsigned long long work = __ballot(busy);
     if (next >= kTasks) {
       if (work == 0ull) break;
     } else if (__popcll(idle) >= RT_POOL_THR || work == 0ull) {
-      // refill: every waiting lane takes the next queued task (rank among the waiting lanes)
+      // refill: every waiting lane publishes its last result and takes the next queued task
+      // (its rank among the waiting lanes), the task's ray and constants as the owner made them
       if (!busy) {
+        publish();
         const uint32_t k = next + __builtin_amdgcn_mbcnt_hi(
                                       (uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         if (k < kTasks) {
           task = k;
-          const double* b = wb + ((k >> 6) - 1u) * kPoolRay * 64u + (k & 63u);
+          const uint32_t row = (k >> 6) - 1u, ow = k & 63u;
+          const double* b = wb + PL::rays + row * kPoolRayD * 64u + ow;
+          const uint32_t* w = wcst + row * kPoolRayW * 64u + ow;
           to = mk(b[0], b[64], b[128]);
           td = mk(b[192], b[256], b[320]);
           ttm = b[384];
-          setup();
+          Cst c;
+          c.ix = __uint_as_float(w[0]), c.iy = __uint_as_float(w[64]), c.iz = __uint_as_float(w[128]);
+          c.nx = __uint_as_float(w[192]), c.ny = __uint_as_float(w[256]), c.nz = __uint_as_float(w[320]);
+          c.oct = w[384];
+          start(c);
           busy = true;
+        } else {
+          task = 0xffffffffu;  // published; nothing left to take
         }
       }
       next += (uint32_t)__popcll(idle);
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (task != 0xffffffffu) publish();  // the last task of every lane that still holds one
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 #pragma unroll
   for (int k = 0; k < NT; ++k) {
     R.t[k] = wb[PL::t + k * 64u + lane];
     R.code[k] = wcode[k * 64u + lane];
   }
-  const double* s = wb + PL::saved + lane;
-  wo = mk(s[0], s[64], s[128]);
-  wd = mk(s[192], s[256], s[320]);
+  const double* sv = wb + PL::saved + lane;
+  wo = mk(sv[0], sv[64], sv[128]);
+  wd = mk(sv[192], sv[256], sv[320]);
 }
 
 template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
@@ -2263,11 +2294,15 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   const bool iso_ref = (P.flags & RT_FLAG_SEMANTICS_REFERENCE) != 0;
   constexpr int NB = BlockOf<BVH>::value;
   // per-lane f64 running sum of the item in flight (the block's samples so far), and of a row
-  // item the row total over its finished blocks (non-BVH kernels: the BVH kernels' LDS holds the
-  // compact trees, and they render no row items)
-  constexpr bool ROWS = !BVH;
+  // item the row total over its finished blocks: static LDS in non-BVH kernels; BVH kernels,
+  // whose LDS holds the compact trees, keep the row totals at the end of the dynamic LDS
+  // (TraceParams::row_lds_off) when the launch's plan has room for them, and otherwise render
+  // no row items (n_pairs_r = 0)
+  constexpr bool ROWS = true;
   __shared__ double sh_acc[3 * NB];
-  __shared__ double sh_row[ROWS ? 3 * NB : 1];
+  __shared__ double sh_row_s[BVH ? 1 : 3 * NB];
+  typedef __attribute__((address_space(3))) double* ldw_t;
+  const ldw_t sh_row = BVH ? (ldw_t)(rt_lds + P.row_lds_off) : (ldw_t)sh_row_s;
   // Non-BVH kernels: a bounce's throughput factor and an ending path's radiance are set inside
   // the divergent shading branches and read after they join; held in registers across the join
   // they were spilled to scratch at five waves per SIMD (cornell_smoke: 30 VGPRs, three

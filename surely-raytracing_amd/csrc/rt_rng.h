@@ -36,7 +36,7 @@ __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint
   if ((v0 | v1 | v2 | v3) == 0u) v0 = 0x9E3779B9u;
   return {v0, v1, v2, v3};
 }
-__device__ __forceinline__ uint32_t rng_u32(Rng& g) {
+__device__ __forceinline__ uint32_t rng_step(Rng& g) {
   uint32_t result = rotl32(g.s1 * 5u, 7) * 9u;
   uint32_t t = g.s1 << 9;
   g.s2 ^= g.s0;
@@ -47,6 +47,19 @@ __device__ __forceinline__ uint32_t rng_u32(Rng& g) {
   g.s3 = rotl32(g.s3, 11);
   return result;
 }
+#ifdef RT_ABL_RNG2
+// ablation build (not shipped): every draw's generator step also runs on a copy of the state,
+// whose result is discarded (same image); the time delta is the generator's cost
+__device__ __forceinline__ uint32_t rng_u32(Rng& g) {
+  Rng c = g;
+  asm volatile("" : "+v"(c.s0), "+v"(c.s1), "+v"(c.s2), "+v"(c.s3));
+  const uint32_t x = rng_step(c);
+  asm volatile("" ::"v"(x), "v"(c.s0), "v"(c.s1), "v"(c.s2), "v"(c.s3));
+  return rng_step(g);
+}
+#else
+__device__ __forceinline__ uint32_t rng_u32(Rng& g) { return rng_step(g); }
+#endif
 // random_double (utils.rs:5-7): 32-bit uniform in [0, 1), exact in f64
 __device__ __forceinline__ double rnd(Rng& g) { return (double)rng_u32(g) * 0x1p-32; }
 // random_range(-1, 1) (utils.rs:9-11): -1 + 2 * (u * 2^-32) = u * 2^-31 - 1, every step exact

@@ -63,6 +63,23 @@ def gather_frame(local, height: int, rank: int, world: int, dst: int = 0):
     return deinterleave(torch.stack(bufs), height, world)
 
 
+GATHER_RCCL = "rt_gather_frame (ncclGather, librtgather.so, include/rt_gather.h)"
+GATHER_TORCH = "torch.distributed.gather"
+
+
+def gather_choice(world: int, rehearse: bool) -> str:
+    """Which frame gather bench.py times at `world` ranks: the product's own C-ABI gather
+    (rt_gather_frame: one ncclGather over RCCL/xGMI + the de-interleave kernel on rank 0) when
+    every rank has its own GPU; torch.distributed.gather over gloo through host memory in the
+    one-GPU rehearsal (RT_BENCH_REHEARSAL=1: RCCL refuses two ranks on one device); none at
+    one rank (the rows are the frame)."""
+    if world <= 1:
+        return "none (one rank renders every row)"
+    if rehearse:
+        return GATHER_TORCH + " (gloo rehearsal on one GPU, through host memory)"
+    return GATHER_RCCL
+
+
 def rank_report(local: dict, rank: int, world: int, dst: int = 0):
     """Every rank's timings (a dict of floats: rt_trace ms, render ms, gather ms, ...) gathered
     to `dst` (torch.distributed.gather_object; outside any timed region). On dst: each key as a

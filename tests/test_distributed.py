@@ -141,3 +141,22 @@ def test_bench_reports_ranks_and_projection_for_n_gpus():
     assert 'res["ranks"] = ranks' in src and "rank_report(" in src
     assert '"scaling_projection"' in src and "projection, not a measurement" in src
     assert "gather_ms" in src and "ev[2].record(stream)" in src
+
+
+def test_bench_gathers_through_the_c_abi_at_n_gpus():
+    """At N > 1 with a GPU per rank bench.py times the product's own gather, rt_gather_frame
+    (librtgather.so: ncclGather + the de-interleave kernel), and names it in the JSON line's
+    "gather" field; the one-GPU gloo rehearsal keeps torch.distributed.gather."""
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo / "surely-raytracing_amd"))
+    from surely_rt.parallel import GATHER_RCCL, gather_choice
+
+    assert gather_choice(8, False) == GATHER_RCCL and "ncclGather" in GATHER_RCCL
+    assert gather_choice(2, True).startswith("torch.distributed.gather (gloo rehearsal")
+    assert gather_choice(1, False).startswith("none")
+    src = (repo / "bench.py").read_text()
+    assert '"gather": gather_name' in src and "rccl.gather(local_buf.data_ptr()" in src
+    assert "RcclFrameGather.unique_id()" in src and "broadcast_object_list" in src

@@ -514,7 +514,8 @@ def test_chunked_and_tail_split_renders_are_bitwise_equal(gpu_available, name, k
     carry the f64 running sums across rt_reduce calls) and the split of a launch's (tile, s_j)
     pairs into row items (the lane forms the row total), segment items (rt_reduce forms it from
     block partials) and per-sample tail items (RT_SEG_PAIRS, RT_TAIL_PAIRS) leave the image bit
-    for bit unchanged. (BVH kernels render no row items: their splits are segment / tail.)"""
+    for bit unchanged. (BVH kernels keep their row totals in the dynamic LDS beside the compact
+    trees: the RT_SEG_PAIRS settings render row items there too.)"""
     blob, cam = rt.preset_blob(name, **kw)
     one = _render_env(blob, cam, {})
     for env in ({"RT_WORKSPACE_MB": 1}, {"RT_TAIL_PAIRS": 0}, {"RT_TAIL_PAIRS": 1 << 30},
@@ -539,6 +540,25 @@ def test_row_items_at_frame_scale_are_bitwise_equal(gpu_available):
     assert st.launches == 1 and rows_only < st.out_bytes < 2 * rows_only, st.out_bytes
     for env in ({"RT_SEG_PAIRS": 1 << 30, "RT_TAIL_PAIRS": 4096},
                 {"RT_SEG_PAIRS": 0, "RT_TAIL_PAIRS": 0}):
+        other = _render_env(blob, cam, env)
+        assert np.array_equal(acc, other, equal_nan=True), env
+
+
+def test_bvh_row_items_at_frame_scale_are_bitwise_equal(gpu_available):
+    """final_scene at 800x800 and 64 spp (80 k (tile, s_j) pairs: the default split renders row
+    items, their row totals in the dynamic LDS after the compact trees and stacks; rt_layout
+    plan_lds): the default split, segment items only, row items only and the BVH kernel without
+    LDS row totals (RT_NO_BVH_ROWS) give the same image bit for bit, and the default's
+    workspace is about one f64 value per (pixel, s_j) (render.rs:185-189)."""
+    blob, cam = rt.preset_blob("final_scene", width=800, spp=64, depth=40)
+    assert cam.sqrt_spp == 8
+    assert rt.lds_check(blob, n_rays=0)["row_lds_off"] != 0xFFFFFFFF
+    acc, st = _gpu(blob, cam)
+    per_value = 64 * 3 * 8  # one 64-pixel slot of f64 RGB
+    rows_only = 800 // 8 * 800 // 8 * cam.sqrt_spp * per_value
+    assert st.launches == 1 and rows_only < st.out_bytes < 1.5 * rows_only, st.out_bytes
+    for env in ({"RT_SEG_PAIRS": 1 << 30, "RT_TAIL_PAIRS": 4096},
+                {"RT_SEG_PAIRS": 0, "RT_TAIL_PAIRS": 0}, {"RT_NO_BVH_ROWS": 1}):
         other = _render_env(blob, cam, env)
         assert np.array_equal(acc, other, equal_nan=True), env
 

@@ -34,7 +34,12 @@ def _assert_walk_invariants(chk, label):
     if chk["cbvh_lds_off"] != 0xFFFFFFFF:  # trees and stacks in LDS: the regions fit the request
         assert chk["cbvh_lds_off"] == chk["stage_bytes"]
         assert chk["stack_lds_off"] == chk["cbvh_lds_off"] + chk["cbvh_bytes"]
-        assert chk["stack_lds_off"] + chk["cbvh_stack"] * chk["block"] == chk["lds_bytes"], (label, chk)
+        stacks_end = chk["stack_lds_off"] + chk["cbvh_stack"] * chk["block"]
+        if chk["row_lds_off"] != 0xFFFFFFFF:  # then the row items' f64 row totals, last
+            assert chk["row_lds_off"] == stacks_end, (label, chk)
+            assert chk["row_lds_off"] + 24 * chk["block"] == chk["lds_bytes"], (label, chk)
+        else:
+            assert stacks_end == chk["lds_bytes"], (label, chk)
         assert chk["lds_total"] <= chk["lds_cu"] == 160 * 1024, (label, chk)
 
 
@@ -51,6 +56,8 @@ def test_final_scene_at_benchmark_size_stages_its_trees():
     _assert_walk_invariants(chk, "final_scene")
     assert chk["trees"] == 2 and chk["block"] == 768
     assert chk["cbvh_lds_off"] != 0xFFFFFFFF
+    # ... and the row totals of its row items (one f64 value per (pixel, s_j): VERDICT r4 item 4)
+    assert chk["row_lds_off"] != 0xFFFFFFFF
     assert 1 <= chk["max_depth"] <= 32
     # the op-counting build and the reference-order flag never stage the compact trees
     for flags in (rt.RT_FLAG_COUNT_OPS, rt.RT_FLAG_REFERENCE_BVH):
