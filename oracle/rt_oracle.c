@@ -201,8 +201,10 @@ static void sincos2pi(double u, double* s, double* c) {
 #define sincos2pi f32_sincos2pi
 #endif
 
-/* =============================================================== RNG (DESIGN.md §4.2)
- * Per pixel-sample stream: pcg4d(pixel, sample, seed_lo, seed_hi) seeds xoshiro128**. */
+/* =============================================================== RNG (DESIGN.md §4.1, §6 S4)
+ * Per pixel-sample stream: pcg4d(pixel, sample, seed_lo, seed_hi) seeds xoroshiro64** (Blackman
+ * and Vigna; 64 bits of state, 32-bit outputs), the device's generator (csrc/rt_rng.h). Until
+ * round 5 both used xoshiro128** (-DORACLE_RNG_X128 / -DRT_RNG_X128 restore it). */
 typedef struct { uint32_t s[4]; } rng_t;
 
 static void pcg4d(uint32_t v[4]) {
@@ -221,9 +223,17 @@ static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 -
 static void rng_seed(rng_t* g, uint64_t seed, uint32_t pixel, uint32_t sample) {
   uint32_t v[4] = {pixel, sample, (uint32_t)seed, (uint32_t)(seed >> 32)};
   pcg4d(v);
+#ifdef ORACLE_RNG_X128
   if ((v[0] | v[1] | v[2] | v[3]) == 0) v[0] = 0x9E3779B9u;
+#else
+  v[0] ^= v[2];  /* xoroshiro64**: the four hash words folded into 64 bits of state */
+  v[1] ^= v[3];
+  v[2] = v[3] = 0;
+  if ((v[0] | v[1]) == 0) v[0] = 0x9E3779B9u;
+#endif
   memcpy(g->s, v, 16);
 }
+#ifdef ORACLE_RNG_X128
 static inline uint32_t rng_u32(rng_t* g) {
   uint32_t* s = g->s;
   uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
@@ -236,6 +246,18 @@ static inline uint32_t rng_u32(rng_t* g) {
   s[3] = rotl32(s[3], 11);
   return result;
 }
+#else
+static inline uint32_t rng_u32(rng_t* g) { /* xoroshiro64** */
+  uint32_t* s = g->s;
+  const uint32_t s0 = s[0];
+  uint32_t s1 = s[1];
+  const uint32_t result = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
+  s1 ^= s0;
+  s[0] = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
+  s[1] = rotl32(s1, 13);
+  return result;
+}
+#endif
 /* random_double (utils.rs:5-7): f64 build (= the device path): 32-bit uniform in [0,1), exact
  * in double; f32 precision-study build: 24-bit uniform (representable in float). */
 #if ORACLE_F64

@@ -557,9 +557,24 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
           << "u, ro, rd, tm, o, d, " << frame << ", tmin, closest, tb, bn, bf, g, C);\n"
           << "      } else {\n  ";
       }
-      o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, "
-        << N[node + 1] << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
-        << ", tmin, closest, tb, bn, bf, g, C);\n";
+      const char* seq_env = std::getenv("RT_SEQ_INF");  // diagnostics: the pooled walks' interval
+      const bool seq_inf = seq_env && *seq_env && *seq_env != '0';
+      if (seq_inf && G.bvh) {
+        // (A/B only: a later subtree walked with tmax = +inf and the list's interval applied
+        // afterwards, as the pooled walks do; measures the culling the tmax = +inf walk loses)
+        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, " << N[node + 1]
+          << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
+          << ", tmin, kInf, tb, bn, bf, g, C);\n"
+          << "      {\n        const bool pf = sub && closest < kInf && fabs(tb - closest) <= closest * (3.0 * kTieRel);\n"
+          << "        sub = sub && tb < closest;\n"
+          << "        if (__ballot(pf) != 0ull && pf)\n"
+          << "          sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, " << N[node + 1]
+          << "u, ro, rd, tm, o, d, " << frame << ", tmin, closest, tb, bn, bf, g, C);\n      }\n";
+      } else {
+        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, "
+          << N[node + 1] << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
+          << ", tmin, closest, tb, bn, bf, g, C);\n";
+      }
       if (j >= 0) o << "      }\n";
       o << "      closest = sub ? tb : closest;\n      code = sub ? " << kBvhCode << "u : code;\n"
         << "      bhn = sub ? bn : bhn;\n      bhf = sub ? bf : bhf;\n    }\n";
@@ -818,6 +833,12 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #endif
 #ifdef RT_ABL_BUDGET
   opts.push_back("-DRT_ABL_BUDGET=" RTJ_STR(RT_ABL_BUDGET));
+#endif
+#ifdef RT_ABL_RNG2
+  opts.push_back("-DRT_ABL_RNG2");
+#endif
+#ifdef RT_RNG_X128
+  opts.push_back("-DRT_RNG_X128");
 #endif
   // diagnostics: extra compiler options, space separated (register-allocation A/B)
   std::vector<std::string> extra;

@@ -1,12 +1,15 @@
-// rt_rng.h — counter-keyed per-sample RNG of the device path (DESIGN.md §4.2).
+// rt_rng.h — counter-keyed per-sample RNG of the device path (DESIGN.md §4.1, §6 S4).
 //
 // The reference draws every random number from rand::thread_rng (ChaCha12, OS-seeded,
 // utils.rs:5-15), so it is unseeded and its draw order depends on rayon scheduling. Here each
 // pixel-sample owns an independent stream keyed by (seed, global pixel index, sample index):
-// pcg4d (Jarzynski & Olano 2020) hashes the key into the state of xoshiro128**; draws are then
-// consumed in exactly the reference's call order. Results are reproducible and independent of
-// how pixels are distributed over lanes, waves or GPUs. The CPU oracle implements the same
-// generator (oracle/rt_oracle.c).
+// pcg4d (Jarzynski & Olano 2020) hashes the key into the state of xoroshiro64** (64 bits of
+// state: two VGPRs); draws are then consumed in exactly the reference's call order. Results are
+// reproducible and independent of how pixels are distributed over lanes, waves or GPUs. The CPU
+// oracle implements the same generator (oracle/rt_oracle.c). Round 5 replaced xoshiro128**
+// (RT_RNG_X128 restores it): the generator step was 8.2 % of C2 and 17.5 % of C3 by the
+// RT_ABL_RNG2 ablation (profiles/r05h_abl_rng_c{2,3}.log), and xoroshiro64**'s shorter step and
+// state took 0.4 % / 0.95 % off their kernel time (profiles/r05h_x64_c{2,3}.log).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,9 +36,29 @@ __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint
   v1 += v2 * v0;
   v2 += v0 * v1;
   v3 += v1 * v2;
+#ifndef RT_RNG_X128
+  // xoroshiro64**: a 64-bit state from the four hash words
+  v0 ^= v2;
+  v1 ^= v3;
+  if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;
+  return {v0, v1, 0u, 0u};
+#else
   if ((v0 | v1 | v2 | v3) == 0u) v0 = 0x9E3779B9u;
   return {v0, v1, v2, v3};
+#endif
 }
+#ifndef RT_RNG_X128
+// xoroshiro64** (Blackman and Vigna): 32-bit outputs from 64 bits of state
+__device__ __forceinline__ uint32_t rng_step(Rng& g) {
+  const uint32_t s0 = g.s0;
+  uint32_t s1 = g.s1;
+  const uint32_t result = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
+  s1 ^= s0;
+  g.s0 = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
+  g.s1 = rotl32(s1, 13);
+  return result;
+}
+#else
 __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   uint32_t result = rotl32(g.s1 * 5u, 7) * 9u;
   uint32_t t = g.s1 << 9;
@@ -47,6 +70,7 @@ __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   g.s3 = rotl32(g.s3, 11);
   return result;
 }
+#endif
 #ifdef RT_ABL_RNG2
 // ablation build (not shipped): every draw's generator step also runs on a copy of the state,
 // whose result is discarded (same image); the time delta is the generator's cost

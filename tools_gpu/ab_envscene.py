@@ -33,7 +33,9 @@ for r in range(ROUNDS):
         acc, st = ds.render(cam, opts)
         if ref is None:
             ref = acc
-        assert np.array_equal(acc, ref, equal_nan=True), f"{spec}: image differs"
+        if os.environ.get("AB_ANY_IMAGE") != "1":  # AB_ANY_IMAGE=1: timing of variants whose
+            # images legitimately differ (another RNG stream)
+            assert np.array_equal(acc, ref, equal_nan=True), f"{spec}: image differs"
         ms.append(st.ms_kernel)
     print(f"round {r}: " + "  ".join(f"{m[-1]:.2f}" for _, _, m in vs), flush=True)
 base = np.median(vs[0][2])
