@@ -484,6 +484,10 @@ __device__ __forceinline__ bool quad_test(Ptr q, d3 o, d3 d, double tmin, double
 // The same test for an axis-aligned quad (rt_layout.h RTL_QUAD_AXIS): bit-identical results,
 // with r = rcp_nr(d) computed once per batch instead of once per quad.
 template <int K>
+struct ic {  // an int as a type (compile-time axis of a generic lambda's argument)
+  static constexpr int value = K;
+};
+template <int K>
 __device__ __forceinline__ double comp(d3 v) {
   return K == 0 ? v.x : (K == 1 ? v.y : v.z);
 }
@@ -1160,6 +1164,62 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <class F>
 __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d, d3 r, double tm,
                                           double tmin, F& cand) {
+#ifdef RT_NO_BOX_LEAF  // A/B: every side of a box leaf tested (the batch loop below)
+  const bool box = false;
+#else
+  const bool box = (rec & RTL_LEAF_BOX) != 0u;
+#endif
+  rec &= ~RTL_LEAF_BOX;
+  if (box && tmin >= 0.0) {
+    // make_box's six sides (object.rs:509-560; rt_obvh.cpp make_box_batch): 0 z = max, 1 x = max,
+    // 2 z = min, 3 x = min, 4 y = max, 5 y = min. The three sides the ray faces (the min side of
+    // an axis where d >= 0) are tested in full with the batch's arithmetic. The other three are
+    // candidates only at their plane's t (aquad_core's quotient, +inf where the plane test or the
+    // interval rejects them), so when every such t lies beyond the facing sides' smallest
+    // candidate by more than the tie window, none of them can win or come within 3 kTieRel of the
+    // final closest (any closest <= that candidate), and their tests are skipped: the walk's result
+    // and tie flag are the full batch's. Otherwise (no facing side hit, a grazing ray, an origin
+    // inside the box) they are tested as well. The order of candidates only matters at exact ties,
+    // which the tie flag sends to the reference-order walk.
+    const gptr B = N + rec + 4;
+    const uint32_t fx = d.x >= 0.0 ? 3u : 1u, fy = d.y >= 0.0 ? 5u : 4u, fz = d.z >= 0.0 ? 2u : 0u;
+    const uint32_t gx = 4u - fx, gy = 9u - fy, gz = 2u - fz;  // the opposite sides
+    double front = kInf;
+    auto side = [&](const AQuad& q, uint32_t f, auto K) {
+      double t;
+      bool inr;
+      aquad_core<decltype(K)::value>(q, o, d, r, t, inr);
+      const double dk = comp<decltype(K)::value>(d);
+      const bool v = !(fabs(dk) < 1e-8) & (tmin <= t) & inr;
+      cand(v, t, rec + 4 + f * RTL_QUAD_WORDS);
+      front = v ? fmin(front, t) : front;
+    };
+    // one side's 64-byte record in flight while the previous one is tested (as the batch loop)
+    AQuad q = load_aquad(B + fx * RTL_QUAD_WORDS), qn = load_aquad(B + fy * RTL_QUAD_WORDS);
+    side(q, fx, ic<0>());
+    q = qn;
+    qn = load_aquad(B + fz * RTL_QUAD_WORDS);
+    side(q, fy, ic<1>());
+    const double px = ldd(B + gx * RTL_QUAD_WORDS, 0), py = ldd(B + gy * RTL_QUAD_WORDS, 0),
+                 pz = ldd(B + gz * RTL_QUAD_WORDS, 0);
+    side(qn, fz, ic<2>());
+    // the opposite sides' candidate t: the plane quotient of aquad_core
+    auto plane = [&](double qk, auto K) {
+      constexpr int k = decltype(K)::value;
+      const double dk = comp<k>(d), rk = comp<k>(r);
+      const double num = qk - comp<k>(o);
+      const double t0 = num * rk;
+      const double t = fma(fma(-dk, t0, num), rk, t0);
+      return (!(fabs(dk) < 1e-8) & (tmin <= t)) ? t : kInf;
+    };
+    const double far = fmin(fmin(plane(px, ic<0>()), plane(py, ic<1>())), plane(pz, ic<2>()));
+    if (!(front < kInf) || far <= front * (1.0 + 3.0 * kTieRel)) {
+      side(load_aquad(B + gx * RTL_QUAD_WORDS), gx, ic<0>());
+      side(load_aquad(B + gy * RTL_QUAD_WORDS), gy, ic<1>());
+      side(load_aquad(B + gz * RTL_QUAD_WORDS), gz, ic<2>());
+    }
+    return;
+  }
   const uint32_t ty = N[rec] & 0xffu;
   if (ty == RTL_SPHERE) {
     const gptr X = N + rec;

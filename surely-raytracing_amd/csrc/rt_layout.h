@@ -104,6 +104,10 @@
  *   level of the deepest tree (child reference | bf16 entry time << 16), header cbvh_stack.
  */
 #define RTL_CBVH_STACK 32
+/* Leaf record words of the OBVH streams and CBVH leaf arrays carry RTL_LEAF_BOX when the record is
+ * a QUADS batch of make_box's six sides in its order (rt_obvh.cpp make_box_batch); the record's
+ * word offset is the low 31 bits. */
+#define RTL_LEAF_BOX 0x80000000u
 #define RTL_BVH_WORDS 16
 /* TRANSLATE / ROTATE_Y (16 words):
  *   [hdr][skip][chain_len][next] [chain0..3: transform nodes root->self] d2-5 p0 p1 p2 0

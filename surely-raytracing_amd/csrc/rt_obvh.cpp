@@ -131,6 +131,25 @@ bool subtree_end(const std::vector<uint32_t>& w, uint32_t x, uint32_t* end) {
   }
 }
 
+// A QUADS batch that is make_box's six sides (object.rs:509-560) in its order: z = max, x = max,
+// z = min, x = min, y = max, y = min, every side axis-aligned in the batch's frame (rt_layout.h
+// RTL_QUAD_AXIS: 3, 1, 3, 1, 2, 2) with the max side's plane above the min side's. Such a leaf is
+// tagged RTL_LEAF_BOX in the ordered BVHs: obvh_leaf tests the three sides the ray faces in full
+// and the other three only when their planes come within the tie window (rt_kernel.h).
+bool make_box_batch(const std::vector<uint32_t>& w, uint32_t x) {
+  if ((w[x] & 0xffu) != RTL_QUADS || (w[x] >> 8) != 6u) return false;
+  static const uint32_t axis[6] = {3u, 1u, 3u, 1u, 2u, 2u};
+  double qk[6];
+  for (int f = 0; f < 6; ++f) {
+    const size_t q = (size_t)x + 4 + (size_t)f * RTL_QUAD_WORDS;
+    if (q + RTL_QUAD_WORDS > w.size() || (w[q] & 0xffu) != RTL_QUAD || RTL_QUAD_AXIS(w[q]) != axis[f])
+      return false;
+    const uint64_t bits = (uint64_t)w[q + 4] | (uint64_t)w[q + 5] << 32;  // d0 = q_k
+    std::memcpy(&qk[f], &bits, 8);
+  }
+  return qk[0] > qk[2] && qk[1] > qk[3] && qk[4] > qk[5];
+}
+
 // leaves of the reference subtree at x (BvhNode children, span-1 duplicates dropped)
 bool collect(const std::vector<uint32_t>& w, uint32_t x, const std::vector<PrimBox>& boxes,
              std::vector<Leaf>& out, int depth) {
@@ -148,7 +167,7 @@ bool collect(const std::vector<uint32_t>& w, uint32_t x, const std::vector<PrimB
   const PrimBox& b = boxes[x];
   if (!b.valid || !b.ref_complete) return false;
   Leaf lf;
-  lf.rec = x;
+  lf.rec = x | (make_box_batch(w, x) ? RTL_LEAF_BOX : 0u);
   lf.b = b;
   for (int k = 0; k < 3; ++k) lf.c[k] = 0.5 * (b.lo[k] + b.hi[k]);
   out.push_back(lf);
@@ -245,7 +264,7 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
       continue;
     if (std::getenv("RT_OBVH_DEBUG")) {  // diagnostics: leaf count, distinct records
       std::vector<uint32_t> r;
-      for (auto& l : leaves) r.push_back(l.rec);
+      for (auto& l : leaves) r.push_back(l.rec & ~RTL_LEAF_BOX);
       std::sort(r.begin(), r.end());
       std::fprintf(stderr, "obvh root %u: %zu leaves, %zu distinct\n", root, leaves.size(),
                    (size_t)(std::unique(r.begin(), r.end()) - r.begin()));
@@ -488,7 +507,7 @@ WalkCheck check_compact_trees(const std::vector<uint32_t>& w, const rtl_scene_he
           ok = false;
           break;
         }
-        const uint32_t rec = T.word(T.n_int * 52u + 4u * li);
+        const uint32_t rec = T.word(T.n_int * 52u + 4u * li) & ~RTL_LEAF_BOX;
         const uint32_t ty = rec < hdr.n_rec_words ? (w[rec] & 0xffu) : 0xffu;
         size_t end = 0;
         if (ty == RTL_QUADS) end = (size_t)rec + 4 + (size_t)(w[rec] >> 8) * RTL_QUAD_WORDS;
