@@ -234,6 +234,9 @@ LdsPlan plan_lds(const rtl_scene_header& hdr, uint32_t o_perl, uint32_t flags, b
   // kernels also the row totals sh_row and the bounce's throughput factor and ending radiance,
   // sh_f / sh_le), the op counters, slack for the profiling build
   L.static_lds = (size_t)L.block * (bvh ? 24 : 96) + 512 + (count ? 128 : 0);
+#ifdef RT_PROF
+  L.static_lds += 4096;  // the profiling build's counters (tools_gpu/prof_*.py)
+#endif
   // a scene whose tables up to the Perlin block fit kStageScene bytes is copied whole (per-lane
   // reads then never leave the CU); otherwise only its first Perlin tables
   const uint32_t used_perlins = hdr.has_textures ? hdr.n_perlins : 0u;
@@ -422,7 +425,7 @@ int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_ray
   const uint64_t v[RT_LDS_CHECK] = {
       (uint64_t)L.block, L.static_lds, L.stage_bytes, L.cbvh_lds_off, L.cbvh_bytes, L.stack_lds_off,
       F.hdr.cbvh_stack, L.lds_bytes, L.static_lds + L.lds_bytes, kLdsTotal, W.trees, W.max_depth,
-      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read, L.row_lds_off};
+      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read, L.row_lds_off, W.grids};
   for (int k = 0; k < n && k < RT_LDS_CHECK; ++k) out[k] = v[k];
   if (msg && msg_len) {
     std::strncpy(msg, W.first_error.c_str(), msg_len - 1);

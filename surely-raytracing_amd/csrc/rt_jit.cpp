@@ -571,8 +571,12 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
           << "          sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, " << N[node + 1]
           << "u, ro, rd, tm, o, d, " << frame << ", tmin, closest, tb, bn, bf, g, C);\n      }\n";
       } else {
-        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, "
-          << N[node + 1] << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
+        // a subtree with a column grid (rt_layout.h GRID, RT_GRID=1) instantiates grid_walk
+        const uint32_t ob = N[node + 3];
+        const bool grid = ob != 0u && (size_t)ob + 8 <= N.size() && N[(size_t)ob + 3] > 4u &&
+                          N[(size_t)ob + 4] != 0u;
+        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH" << (grid ? ", true" : "") << ">(P, "
+          << node << "u, " << N[node + 1] << "u, " << ob << "u, ro, rd, tm, o, d, " << frame
           << ", tmin, closest, tb, bn, bf, g, C);\n";
       }
       if (j >= 0) o << "      }\n";

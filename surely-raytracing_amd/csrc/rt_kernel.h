@@ -922,7 +922,9 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
 
 // A BVH subtree [node, stop) walked per lane: its ordered BVH when it has one (obvh != 0),
 // otherwise (and always in the op-counting build) the reference tree in the reference order.
-template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
+// GRID: the subtree may have a column grid (rt_layout.h GRID, RT_GRID=1 scenes): set by the
+// generated walker for exactly those subtrees, so no other kernel carries grid_walk's code.
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH, bool GRID = false>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
@@ -1635,6 +1637,160 @@ __device__ __forceinline__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, 
                                                 hit_node, hit_frame, flag);
 }
 
+// ---------------------------------------------------------------- column grid walk
+// A BVH subtree whose leaves each lie in one cell of a regular grid over x and z (rt_layout.h
+// GRID; final_scene's ground: 20 x 20 boxes of random height) is walked by marching the ray
+// through the grid's columns along its major axis instead of stepping the tree: per column the
+// minor cells the ray can be in (1 to 3) and, for each whose leaf top lies above the ray's lowest
+// point in the column, the leaf's exact test (obvh_leaf) with cbvh_walk_t's candidate logic and
+// tie flag. The march is conservative: every position is widened by a margin m (the grid's own
+// tolerance plus 2^-18 of the coordinates' magnitude, far above the f32 roundings), so every cell
+// whose leaf can hold a candidate at t <= closest (1 + 4 kTieRel) is tested, and the columns stop
+// once the next one starts beyond that. The result and flag are therefore cbvh_walk_t's: the same
+// smallest candidate, the same two smallest values of {tmax, candidates} within the tie window.
+template <bool MAIN>
+__device__ bool grid_walk(const TraceParams& P, uint32_t gb, d3 o, d3 d, double tm, int frame,
+                          double tmin, double tmax, double& t_out, uint32_t& hit_node,
+                          int& hit_frame, bool& flag) {
+  const gptr N = (gptr)P.nodes;
+  const kptr G = (kptr)P.nodes + gb;
+  auto gf = [&](int k) { return __uint_as_float(G[k]); };
+  const uint32_t nx = G[0], nz = G[1];
+  const float X0 = gf(4), Z0 = gf(5), Wx = gf(6), Wz = gf(7), iWx = gf(8), iWz = gf(9);
+  const float Ylo = gf(10), Yhi = gf(11), mg = gf(12);
+  typedef uint32_t v2u_t __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(3))) v2u_t* lc_t;
+  const lc_t cells = (lc_t)(rt_lds + P.cbvh_lds_off + G[2]);  // staged with the compact trees
+  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+  const float m = fmaf(fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))), 0x1p-18f, mg);
+  double closest = tmax, second = kInf;
+  bool hit = false;
+  uint32_t hn = 0;
+  auto cand = [&](bool valid, double t, uint32_t rec) {  // cbvh_walk_t's
+    const double te = valid ? t : kInf;
+    second = fmin(second, fmax(closest, te));
+    const bool win = te < closest;
+    closest = win ? te : closest;
+    hn = win ? rec : hn;
+    hit = hit | win;
+  };
+  // the cut: an f32 bound >= closest (1 + 4 kTieRel)
+  float cut = (float)(closest + closest * 0x1p-20);
+  // the grid's box widened by m: [t0, t1]
+  const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy),
+              idz = __builtin_amdgcn_rcpf(dz);
+  // entry and exit times of [lo, hi] by the sign of 1/d (as the octant's near and far bounds): a
+  // NaN time (0 * inf, the origin on a bound of an axis the ray runs parallel to) stays NaN and
+  // constrains nothing in the fmaxf / fminf below
+  auto slab = [](float lo, float hi, float oo, float id, float& tn, float& tf) {
+    const float a = (lo - oo) * id, b = (hi - oo) * id;
+    const bool neg = id < 0.0f;
+    tn = neg ? b : a;
+    tf = neg ? a : b;
+  };
+  float tnx, tfx, tny, tfy, tnz, tfz;
+  slab(X0 - m, fmaf((float)nx, Wx, X0) + m, ox, idx, tnx, tfx);
+  slab(Ylo - m, Yhi + m, oy, idy, tny, tfy);
+  slab(Z0 - m, fmaf((float)nz, Wz, Z0) + m, oz, idz, tnz, tfz);
+  const float t0 = fmaxf(fmaxf((float)(tmin - fabs(tmin) * 0x1p-20), tnx), fmaxf(tny, tnz));
+  const float t1 = fminf(tfx, fminf(tfy, tfz));
+  // the major axis a (x when the ray crosses columns of x at least as fast as rows of z). One
+  // march with the ray's per-axis values selected per lane: instantiating it per major axis runs
+  // the two instances (and their leaf tests) one after the other in a wave whose lanes differ
+  // (C4 +18.8 %, profiles/r05n_ab_grid_peraxis.log).
+  const bool xa = fabsf(dx) * Wz >= fabsf(dz) * Wx;
+  const float oa = xa ? ox : oz, da = xa ? dx : dz, ida = xa ? idx : idz;
+  const float ob = xa ? oz : ox, db = xa ? dz : dx, idb = xa ? idz : idx;
+  const float A0 = xa ? X0 : Z0, Wa = xa ? Wx : Wz, iWa = xa ? iWx : iWz;
+  const float B0 = xa ? Z0 : X0, Wb = xa ? Wz : Wx, iWb = xa ? iWz : iWx;
+  const int na = (int)(xa ? nx : nz), nb = (int)(xa ? nz : nx);
+  const uint32_t sa = xa ? nz : 1u, sb = xa ? 1u : nz;  // cell = i_x nz + i_z
+  // columns in the order the ray's times of them increase (by the sign of 1/d_a, so a vertical
+  // ray's -0 runs downwards); the first one holds the ray's position at t0 moved back by m
+  const int step = ida < 0.0f ? -1 : 1, jstep = idb < 0.0f ? -1 : 1;
+  const float pa = fmaf(t0, da, oa);
+  int ia = (int)floorf(((step > 0 ? pa - m : pa + m) - A0) * iWa);
+  ia = min(max(ia, 0), na - 1);
+#ifdef RT_PROF
+  uint32_t pf_box = 0, pf_leaf = 0;
+  const unsigned long long pf_t0 = __builtin_readcyclecounter();
+#endif
+  // Per column, in the order the ray reaches them, the minor cells it can be in over the
+  // column's interval [ta, tb]; per cell its own interval (widened by m as the columns) against
+  // the cut, and the ray's lowest y over it against the top of the cell's leaf; then the leaf.
+  // (tend = min(t1, cut): the cut, tightened by the grid's exit. The while-while form of
+  // cbvh_walk_t, leaves of all lanes together after each lane's advance, measured +8.4 % in one
+  // A/B whose log was overwritten.)
+  float tend = fminf(t1, cut);
+  if (t0 <= tend) {
+    for (; ia >= 0 && ia < na; ia += step) {
+      const float lo = fmaf((float)ia, Wa, A0) - m, hi = fmaf((float)(ia + 1), Wa, A0) + m;
+      float tin, tout;
+      slab(lo, hi, oa, ida, tin, tout);
+      const float ta = fmaxf(t0, tin);
+      if (ta > tend) break;  // this column (and every later one) starts past the cut
+      const float tb = fminf(tend, tout);
+#ifdef RT_PROF
+      ++pf_box;
+#endif
+      if (!(ta <= tb)) continue;  // the ray left this column before t0
+      const float pb0 = fmaf(ta, db, ob), pb1 = fmaf(tb, db, ob);
+      const int jb0 = max((int)floorf((fminf(pb0, pb1) - m - B0) * iWb), 0);
+      const int jb1 = min((int)floorf((fmaxf(pb0, pb1) + m - B0) * iWb), nb - 1);
+      for (int k = 0, j = jstep > 0 ? jb0 : jb1; k <= jb1 - jb0; ++k, j += jstep) {
+        float tcin, tcout;
+        slab(fmaf((float)j, Wb, B0) - m, fmaf((float)(j + 1), Wb, B0) + m, ob, idb, tcin, tcout);
+        const float tc = fmaxf(ta, tcin), td = fminf(fminf(tb, tend), tcout);
+        if (!(tc <= td)) continue;
+        const float ylo = fminf(fmaf(tc, dy, oy), fmaf(td, dy, oy)) - m;
+        const v2u_t c = cells[(uint32_t)ia * sa + (uint32_t)j * sb];
+        if (!(ylo <= __uint_as_float(c.x))) continue;
+#ifdef RT_PROF
+        ++pf_leaf;
+#endif
+        const double closest_before = closest;
+        obvh_leaf(N, c.y, o, d, r, tm, tmin, cand);
+        if (closest != closest_before) tend = fminf(tend, (float)(closest + closest * 0x1p-20));
+      }
+    }
+  }
+  flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
+         (hit & (closest <= tmin * (1.0 + kTieRel)));
+#ifdef RT_PROF
+  {
+    const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
+    uint32_t mb = pf_box, ml = pf_leaf, sbx = pf_box, sl = pf_leaf;
+    for (int k = 32; k > 0; k >>= 1) {
+      mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
+      ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
+      sbx += (uint32_t)__shfl_xor((int)sbx, k);
+      sl += (uint32_t)__shfl_xor((int)sl, k);
+    }
+    unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
+    const unsigned long long fl = __popcll(__ballot(flag));
+    if (prof_first_lane()) {
+      atomicAdd(&pc[0], (unsigned long long)sbx);
+      atomicAdd(&pc[2], (unsigned long long)sl);
+      atomicAdd(&pc[1], (unsigned long long)mb);
+      atomicAdd(&pc[3], (unsigned long long)ml);
+      atomicAdd(&pc[4], 1ull);
+      atomicAdd(&pc[5], dt);
+      atomicAdd(&P.ops[52], fl);
+    }
+  }
+#endif
+  if (hit) {
+    t_out = closest;
+    if (MAIN) {
+      hit_node = hn;
+      hit_frame = frame;
+    }
+  }
+  return hit;
+}
+
 // ---------------------------------------------------------------- pooled BVH walks
 // A world query visits every top-level BVH subtree of the list (hittable.rs:88-109 ->
 // BvhNode::hit :216-236), and each walk runs until the wave's slowest lane is done: at C4 the
@@ -1882,7 +2038,7 @@ __device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd
   wd = mk(sv[192], sv[256], sv[320]);
 }
 
-template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH, bool GRID>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
@@ -1907,8 +2063,11 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
     if (obvh != 0u && !(P.flags & RT_FLAG_REFERENCE_BVH)) {
       bool flag = false;
       const uint4 hd = ld4u((gptr)P.nodes + obvh);  // [n_entries][cbvh block][root ref][streams]
+      const uint32_t grid = GRID && hd.w > 4u ? ((gptr)P.nodes)[obvh + 4] : 0u;
       bool h;
-      if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
+      if (GRID && grid != 0u && P.cbvh_lds_off != ~0u)  // the column grid in LDS
+        h = grid_walk<MAIN>(P, grid, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
+      else if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
         h = cbvh_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
       else
         h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,

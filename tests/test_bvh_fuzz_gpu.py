@@ -116,3 +116,92 @@ def test_dense_bvh_scene_parity(gpu_available, seed):
     ref = _render_env(blob, cam, {}, flags=rt.RT_FLAG_OVERWRITE | rt.RT_FLAG_REFERENCE_BVH)
     assert np.array_equal(lds, streams, equal_nan=True)
     assert np.array_equal(lds, ref, equal_nan=True)
+
+
+def column_grid_scene(seed, parts="gsimdc"):
+    """A BVH of leaves on a regular x/z lattice (rt_layout.h GRID, walked by rt_kernel.h grid_walk
+    under RT_GRID=1; final_scene's ground, book2 main.rs, is the benchmark case): boxes touching their neighbours
+    (shared side planes), heights drawn from a few values (coplanar tops across cells), spheres
+    inside cells, empty cells (cell sizes, origins and most heights dyadic, so that shared
+    planes are one double), and the same kind of grid again inside a RotateY + Translate
+    instance. The camera looks along the grid at a grazing angle, so walks cross many columns, and
+    scattered rays start on the box tops and sides. parts (a diagnostic can drop some): g the main
+    grid, s its spheres, i the instance; m, d, c: metal, dielectric, checker-textured items
+    (without them, the two plain Lambertians)."""
+    rnd = np.random.default_rng(2000 + seed)
+    sc = rt.Scene(seed)
+    u = lambda a, b: float(rnd.uniform(a, b))  # noqa: E731
+    col = lambda: tuple(float(x) for x in rnd.uniform(0.1, 0.9, 3))  # noqa: E731
+    light = sc.diffuse_light((12.0, 12.0, 12.0))
+    # (the checker's period is not a multiple of the lattice's, for the same reason as below)
+    mats = [sc.lambertian(col()), sc.lambertian(col()), sc.metal(col(), u(0.0, 0.3)),
+            sc.dielectric(1.5), sc.lambertian(tex=sc.checker_from_color(0.2718281828, col(), col()))]
+    allowed = [0, 1] + [k for k, p in ((2, "m"), (3, "d"), (4, "c")) if p in parts]
+    pick = lambda: mats[allowed[int(rnd.integers(0, 5)) % len(allowed)]]  # noqa: E731
+
+    def grid(nx, nz, w, x0, z0, y0=0.0625):
+        heights = [float(rnd.integers(3, 17)) / 8 for _ in range(3)]  # dyadic: exact planes
+        items = []
+        for i in range(nx):
+            for j in range(nz):
+                a, b = x0 + i * w, z0 + j * w
+                corner = (i, j) in ((0, 0), (nx - 1, nz - 1))
+                kind = 0.0 if corner else rnd.uniform()
+                if kind < 0.6 or i == j:  # a box filling the cell (every row and column has one)
+                    h = heights[int(rnd.integers(0, 3))] if rnd.uniform() < 0.7 else u(0.1, 2.5)
+                    items.append(sc.make_box((a, y0, b), (a + w, h, b + w), pick()))
+                elif kind < 0.8:
+                    r = u(0.1, 0.45) * w
+                    c = (a + 0.5 * w, y0 + r + u(0.0, 1.0), b + 0.5 * w)
+                    if "s" in parts:
+                        items.append(sc.sphere(c, r, pick()))
+        return sc.create_bvh(sc.hittable_list(*items))
+
+    # dyadic cell sizes and origins: neighbours' shared planes are the same double, as in
+    # final_scene's integer lattice; no face on a coordinate plane (x, y or z = 0 is a boundary
+    # of the checker, floor(p / scale), where the sign of the hit point's last bit decides)
+    nx, nz = int(rnd.integers(5, 13)), int(rnd.integers(5, 13))
+    w = float(rnd.integers(4, 10)) / 8
+    main = grid(nx, nz, w, (0.5 - np.floor(4 * nx * w)) / 8, (0.5 - np.floor(4 * nz * w)) / 8)
+    inst = sc.translate(sc.rotate_y(grid(6, 5, 0.375, -1.0625, -0.9375), u(-50, 50)),
+                        (u(-2, 2), 2.6, u(-2, 2)))
+    world = ([main] if "g" in parts else []) + ([inst] if "i" in parts else [])
+    world.append(sc.quad((-30, -0.01, -30), (60, 0, 0), (0, 0, 60), mats[0]))
+    world.append(sc.quad((-1, 9, -1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((-1, 9, -1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(sc.hittable_list(*world), lights)
+    look_from = (-0.6 * nx * w, u(1.0, 3.0), -0.6 * nz * w)
+    cam = rt.camera_new(1.0, 64, 16, 12, 60, look_from, (0.3 * nx * w, 0.5, 0.3 * nz * w),
+                        (0, 1, 0), 0, 0, (0.5, 0.6, 0.8) if seed % 2 else (0.0, 0.0, 0.0))
+    return blob, cam
+
+
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_column_grid_scene_parity(gpu_available, seed):
+    """The column-grid walk (RT_GRID=1 at scene creation, opt-in) bit for bit against every
+    other walk of the same trees: the compact-tree walk (the default), the global streams, the
+    reference-order walk (RT_FLAG_REFERENCE_BVH; the op-counting build always walks it) and the
+    interpreter kernel; and the default walks against the f64 oracle as the dense scenes
+    (_compare: per pixel within TOL, every path decision's op count identical, the box-culling
+    counters within CULL_RTOL)."""
+    import os
+
+    blob, cam = column_grid_scene(seed)
+    os.environ["RT_GRID"] = "1"
+    try:
+        assert rt.lds_check(blob, n_rays=0)["grids"] == 2
+    finally:
+        del os.environ["RT_GRID"]
+    acc_g, _, st = _compare(blob, cam, check_ops=False)
+    assert np.isfinite(acc_g).any() and acc_g[np.isfinite(acc_g)].mean() > 0.0
+    _, ops_o = O.render(blob, cam, rt.make_opts(cam, seed=1, flags=rt.RT_FLAG_OVERWRITE),
+                        precision=64)
+    ops_g = st.op_counts()
+    path = {k: (ops_g[k], ops_o[k]) for k in ops_o if k not in CULL_OPS and ops_g[k] != ops_o[k]}
+    assert not path, path
+    g = _render_env(blob, cam, {"RT_GRID": 1})
+    for env, flags in (({}, None), ({"RT_NO_CBVH_LDS": 1}, None),
+                       ({"RT_GRID": 1}, rt.RT_FLAG_OVERWRITE | rt.RT_FLAG_INTERPRETER),
+                       ({}, rt.RT_FLAG_OVERWRITE | rt.RT_FLAG_REFERENCE_BVH)):
+        other = _render_env(blob, cam, env, **({"flags": flags} if flags else {}))
+        assert np.array_equal(g, other, equal_nan=True), (env, flags)

@@ -23,7 +23,8 @@ opts = rt.make_opts(cam, seed=1)
 for rep in range(2):
     acc = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
     st = rt.RtStats()
-    assert lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st)) == 0
+    rc = lib.rt_render(h, C.byref(cam), C.byref(opts), acc.ctypes.data, C.byref(st))
+    assert rc == 0, (rc, lib.rt_last_error())
 cyc = np.array([st.ops[k] for k in range(8)], dtype=np.float64)
 pc = (C.c_uint64 * 24)()
 assert lib.rt_scene_prof_counters(h, pc, 24) == 0
