@@ -1440,13 +1440,22 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
   const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 4u * threadIdx.x;
   const uint32_t sstep = 4u * blockDim.x;
   auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
+  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
+#ifdef RT_OLD_INV  // A/B: the slab reciprocals from their own rcp + two Newton steps
   const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
   const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
-  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
+  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
+#else
+  // The f32 slab reciprocals from the leaves' f64 ones (rcp_nr1, within an ulp of 1/d, then
+  // rounded to f32 like 1/d itself: inside the box test's 2^-18 budget). d_a = +-0 gives NaN
+  // there (rcp_nr1's 0 * inf), and a NaN slab time constrains nothing: every box is kept on
+  // that axis, never dropped. The octant is d's sign bit (-0: the d_a < 0 side, as 1/-0 = -inf).
+  const bool nx = __builtin_signbit(d.x), ny = __builtin_signbit(d.y), nz = __builtin_signbit(d.z);
+  const float ix = (float)r.x, iy = (float)r.y, iz = (float)r.z;
+#endif
   constexpr float kBoxRel = 0x1p-20f;
   constexpr float kBoxPos = 1.0f + 0x1p-18f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
   // slab times as fma(bound, inv, -o inv): one packed fma per axis instead of a subtraction and
   // a product. The extra rounding of o inv is 2^-24 |o inv| <= 2^-24 (|bound| + |bound - o|) |inv|,
   // the same two parts as o's own rounding (obvh_walk's budget): inside the bounds' margin and
