@@ -26,6 +26,8 @@ Also reported (one JSON line on rank 0):
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--width 800] [--spp 1000]
        torchrun --nproc-per-node N bench.py --gpus N ...
+At --gpus N > 1 without torchrun (WORLD_SIZE unset) the script starts its N ranks itself
+(self_launch: one child process per GPU, torchrun's environment, rank 0's line relayed).
 """
 import argparse
 import json
@@ -74,6 +76,8 @@ def parse():
                     help="target CPU-baseline work (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the op-count pass")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="check the N-rank launch over gloo without a GPU (no render)")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     for k in ("scene", "width", "spp", "depth"):
@@ -139,8 +143,94 @@ def cpu_baseline(blob, cam, seed, target_s):
     }
 
 
+def self_launch(n: int, argv) -> int:
+    """`python3 bench.py --gpus N` without torchrun (WORLD_SIZE unset, N > 1): start N child
+    processes of this same script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT set as torchrun would, relay rank 0's stdout (its JSON line) and
+    return non-zero if any rank fails. The parent never imports torch nor touches the GPU, and
+    it starts children (no exec), so this is safe on the GPU box. A rank that fails ends the
+    others (they would wait in a barrier forever): exact child PIDs, SIGTERM then SIGKILL."""
+    import socket
+    import subprocess
+    import threading
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve())]
+                                      + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None))
+
+    def relay(stream):
+        for line in iter(stream.readline, b""):
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+
+    t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    t.start()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad[0]
+            print(f"bench.py self-launch: rank {bad[0][0]} exited with {bad[0][1]}; "
+                  "ending the other ranks", file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 20
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        if all(c is not None for c in (p.poll() for p in procs)):
+            break
+        time.sleep(0.2)
+    t.join(timeout=10)
+    if failed is not None:
+        return failed[1] if failed[1] > 0 else 1
+    return 0
+
+
+def launch_check(args):
+    """--launch-check: the self-launch's rank plumbing without a GPU (gloo): every rank joins the
+    process group from the environment the launcher set, takes the max over ranks as the bench
+    does, and rank 0 prints one JSON line. Used by the CPU test of the launcher."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("RT_LAUNCH_CHECK_FAIL_RANK") == str(rank):
+        raise SystemExit(3)  # the launcher's failure path: the other ranks wait in rendezvous
+    dist.init_process_group("gloo")
+    dist.barrier()
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    objs = [None] * world if rank == 0 else None
+    dist.gather_object({"rank": rank, "local_rank": int(os.environ["LOCAL_RANK"])}, objs, dst=0)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "max_over_ranks": t.item(),
+                          "ranks": objs}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's plain `python3 bench.py --gpus N`: become the launcher of N ranks
+        raise SystemExit(self_launch(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        return launch_check(args)
     import torch
     import torch.distributed as dist
 

@@ -213,17 +213,16 @@ int rt_scene_validate(const rt_scene_blob* blob);
 int rt_scene_layout_stats(const rt_scene_blob* blob, uint32_t* out, int n);
 
 /* Host-only check of a product render's LDS plan and of the compact BVHs its walk reads from LDS
- * (no device needed): out[0..19] = workgroup size, static LDS bound, staged table
+ * (no device needed): out[0..18] = workgroup size, static LDS bound, staged table
  * bytes, compact-tree LDS offset (0xffffffff: not in LDS), compact-tree bytes, stack LDS offset,
  * stack bytes per lane (header cbvh_stack), dynamic LDS, static + dynamic, the CU's LDS, compact
  * trees, deepest tree (internal nodes, root = 1), structural errors, largest stack slot the
  * walk stores to, largest number of pending entries, rays walked, box steps, one past the
  * largest compact-region byte read, the row totals' LDS offset (0xffffffff: the launch renders
- * no row items), column grids (rt_layout.h GRID; their cells' leaf records are checked with the
- * trees' and count in the structural errors). The walks are a host restatement of the LDS walk over
+ * no row items). The walks are a host restatement of the LDS walk over
  * n_rays random rays per tree without closest-hit culling (the worst case for the stack).
  * msg (may be NULL) receives the first structural error. `flags`: the render's RT_FLAG_*. */
-#define RT_LDS_CHECK 20
+#define RT_LDS_CHECK 19
 int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_rays, uint64_t seed,
                        uint64_t* out, int n, char* msg, uint32_t msg_len);
 

@@ -50,7 +50,7 @@ pub const RT_FLAG_INTERPRETER: u32 = 0x8;
 pub const RT_FLAG_REFERENCE_BVH: u32 = 0x10;
 
 pub const RT_LAYOUT_STATS: c_int = 11;
-pub const RT_LDS_CHECK: c_int = 20;
+pub const RT_LDS_CHECK: c_int = 19;
 pub const RT_TRACE_HISTORY: c_int = 64;
 
 #[repr(C)]

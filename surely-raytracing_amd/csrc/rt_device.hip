@@ -283,16 +283,6 @@ LdsPlan plan_lds(const rtl_scene_header& hdr, uint32_t o_perl, uint32_t flags, b
 struct TableLayout {
   size_t o_nodes = 0, o_mats = 0, o_texs = 0, o_lig = 0, o_loff = 0, o_perl = 0, o_tx = 0, total = 0;
 };
-// Bytes of TraceParams::pool for `waves` resident waves of a walker with `nt` pooled trees.
-size_t pool_bytes(int nt, size_t waves) {
-  switch (nt) {
-    case 2: return waves * PoolLayout<2>::doubles * sizeof(double);
-    case 3: return waves * PoolLayout<3>::doubles * sizeof(double);
-    case 4: return waves * PoolLayout<4>::doubles * sizeof(double);
-    default: return 0;
-  }
-}
-
 TableLayout table_layout(const rtf::FlatScene& F) {
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   TableLayout T;
@@ -318,8 +308,6 @@ TableLayout table_layout(const rtf::FlatScene& F) {
 struct RenderSlot {
   uint8_t* work = nullptr;  // row totals / segment partials / tail samples + f64 running sums
   size_t work_bytes = 0;
-  double* pool = nullptr;   // pooled BVH walks' exchange (rt_kernel.h cbvh_pool)
-  size_t pool_bytes = 0;
   unsigned long long* ops = nullptr;  // 32 op counters, the pool-queue word (32), profiling (40..)
   unsigned int* queue = nullptr;
   hipEvent_t done = nullptr;  // recorded after the render's last kernel
@@ -353,7 +341,6 @@ struct rt_scene {
   // generated (jit_msg says why), -2 = compile failed (jit_msg = log; the interpreter runs)
   std::string jit_walker, jit_msg;
   int jit_state = -1;
-  int pool_trees = 0;  // BVH subtrees the generated walker walks as one pool (rt_jit.hpp generate)
   rtj::Kernel jit_k[4];  // [tex][staged]
   // rt_trace launch timing: one event pair per launch, ring of kTraceRing, tagged by render id
   static constexpr int kTraceRing = 4 * RT_TRACE_HISTORY;
@@ -425,7 +412,7 @@ int rt_scene_lds_check(const rt_scene_blob* blob, uint32_t flags, uint32_t n_ray
   const uint64_t v[RT_LDS_CHECK] = {
       (uint64_t)L.block, L.static_lds, L.stage_bytes, L.cbvh_lds_off, L.cbvh_bytes, L.stack_lds_off,
       F.hdr.cbvh_stack, L.lds_bytes, L.static_lds + L.lds_bytes, kLdsTotal, W.trees, W.max_depth,
-      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read, L.row_lds_off, W.grids};
+      W.errors, W.max_store_slot, W.max_live, W.rays, W.steps, W.max_read, L.row_lds_off};
   for (int k = 0; k < n && k < RT_LDS_CHECK; ++k) out[k] = v[k];
   if (msg && msg_len) {
     std::strncpy(msg, W.first_error.c_str(), msg_len - 1);
@@ -518,7 +505,7 @@ int rt_scene_create(const rt_scene_blob* blob, int device, rt_scene** out) {
   if (jit_env && std::strcmp(jit_env, "0") == 0) {
     sc->jit_msg = "disabled by RT_JIT=0";
   } else {
-    sc->jit_walker = rtj::generate(F, &sc->jit_msg, &sc->pool_trees);
+    sc->jit_walker = rtj::generate(F, &sc->jit_msg);
     sc->jit_state = sc->jit_walker.empty() ? -1 : 0;
   }
   sc->sphere_light0 = -1;
@@ -544,7 +531,6 @@ void rt_scene_destroy(rt_scene* sc) {
   if (sc->dev) (void)hipFree(sc->dev);
   for (const auto& sl : sc->slots) {
     if (sl->work) (void)hipFree(sl->work);
-    if (sl->pool) (void)hipFree(sl->pool);
     if (sl->ops) (void)hipFree(sl->ops);
     if (sl->done) (void)hipEventDestroy(sl->done);
     if (sl->ev0) (void)hipEventDestroy(sl->ev0);
@@ -978,21 +964,6 @@ static int render_device_rows(rt_scene* sc, const rt_camera* cam, const rt_rende
   }
   double* tot = (double*)sl->work;
   P.part = (double*)(sl->work + tot_bytes);
-  // the pooled BVH walks' exchange blocks, one per resident wave (only a scene-specialised kernel
-  // with pooled walks and the compact trees in LDS uses them)
-  P.pool = nullptr;
-  if (jfn && sc->pool_trees >= 2 && P.cbvh_lds_off != ~0u) {
-    const size_t pb = pool_bytes(sc->pool_trees, (size_t)max_blocks * (block / 64));
-    if (pb > sl->pool_bytes) {
-      if (sl->recorded) HIP_TRY(hipEventSynchronize(sl->done));
-      if (sl->pool) HIP_TRY(hipFree(sl->pool));
-      sl->pool = nullptr;
-      sl->pool_bytes = 0;
-      HIP_TRY(hipMalloc(&sl->pool, pb));
-      sl->pool_bytes = pb;
-    }
-    P.pool = sl->pool;
-  }
   hold.stream = stream;
   hold.enqueued = true;  // from here on a failure still records `done` (SlotHold)
   if (ops_buf) HIP_TRY(hipMemsetAsync(sl->ops, 0, sizeof(unsigned long long) * 32, stream));

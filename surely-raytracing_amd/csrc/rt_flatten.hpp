@@ -56,7 +56,6 @@ struct WalkCheck {
   uint32_t max_live = 0;        // largest number of pending entries
   uint64_t rays = 0, steps = 0;  // walks emulated, box steps taken
   uint64_t max_read = 0;        // one past the largest CBVH-region byte read
-  uint32_t grids = 0;           // column grids (rt_layout.h GRID), checked like the leaf arrays
   std::string first_error;
 };
 WalkCheck check_compact_trees(const std::vector<uint32_t>& nodes, const rtl_scene_header& hdr,

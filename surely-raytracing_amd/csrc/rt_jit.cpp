@@ -378,9 +378,8 @@ bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string*
 
 }  // namespace
 
-std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees) {
+std::string generate(const rtf::FlatScene& F, std::string* why) {
   const std::vector<uint32_t>& N = F.nodes;
-  if (pool_trees) *pool_trees = 0;
   if (F.hdr.nested_volumes) {
     *why = "ConstantMedium nested in a volume boundary: the interpreter kernel walks it";
     return "";
@@ -389,60 +388,6 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
     *why = "node array too large for the packed winner code";
     return "";
   }
-  // The top level's BVH subtrees with a compact ordered BVH (rt_layout.h CBVH), in list order,
-  // each with its frame and the frame's transform chain (root first): 2 to 4 of them are walked
-  // as one pool per wave before the list (rt_kernel.h cbvh_pool).
-  struct PoolTree {
-    size_t node;
-    int frame;
-    std::vector<size_t> chain;
-  };
-  std::vector<PoolTree> pool;
-  {
-    auto chain_of = [&](int fr) {
-      std::vector<size_t> c;
-      if (fr < 0) return c;
-      const uint32_t len = N[(size_t)fr + 2];
-      const bool lng = (N[(size_t)fr] & RTL_XFORM_LONG) != 0u;
-      for (uint32_t k = 0; k < len; ++k)
-        c.push_back(lng ? N[(size_t)N[(size_t)fr + 4] + k] : N[(size_t)fr + 4 + k]);
-      return c;
-    };
-    size_t x = F.hdr.root;
-    int fr = -1;
-    for (size_t guard = 0; x + 4 <= N.size() && guard <= N.size(); ++guard) {
-      const uint32_t ty = N[x] & 0xffu;
-      if (ty == RTL_END) break;
-      if (ty == RTL_TRANSLATE || ty == RTL_ROTATE_Y) {
-        fr = (int)x;
-        x = N[x + 3];
-      } else if (ty == RTL_EXIT) {
-        fr = (int)N[x + 2];
-        x = N[x + 3];
-      } else if (ty == RTL_BVH) {
-        const uint32_t ob = N[x + 3];
-        if (ob != 0u && (size_t)ob + 4 <= N.size() && N[(size_t)ob + 1] != 0xffffffffu)
-          pool.push_back({x, fr, chain_of(fr)});
-        x = N[x + 1];
-      } else if (ty == RTL_QUAD || ty == RTL_SPHERE) {
-        x = N[x + 3];
-      } else {
-        x = N[x + 1];  // QUADS, VOLUME, DUP, OTHER: their skip
-      }
-    }
-    // opt-in (RT_POOL=1 at scene creation): measured slower at C4 (DESIGN.md §4.1c "Pooled
-    // walks": +14 % kernel time, lane utilisation 0.334 -> 0.379 but 28 % more lane work)
-    const char* on = std::getenv("RT_POOL");
-    if (pool.size() < 2 || !(on && *on && *on != '0')) pool.clear();
-    if (pool.size() > 4) pool.resize(4);
-  }
-  const int NT = (int)pool.size();
-  if (pool_trees) *pool_trees = NT;
-  auto pool_index = [&](size_t nd) {
-    for (int j = 0; j < NT; ++j)
-      if (pool[j].node == nd) return j;
-    return -1;
-  };
   Gen G(N);
   std::ostringstream& o = G.o;
   std::ostringstream pre;  // policies the walker refers to (generated volume boundary queries)
@@ -460,30 +405,6 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
        "    uint32_t bhn = 0u;   // BVH subtree winner (code == kBvhCode)\n"
        "    int bhf = -1;\n"
        "    d3 o = ro, d = rd;\n";
-  if (NT) {
-    // the pooled walks (rt_kernel.h cbvh_pool) when this render has the compact trees in LDS and
-    // a pool buffer; every lane of the wave runs the world query (trace_body)
-    o << "    PoolOut<" << NT << "> pw;\n"
-      << "    const bool pooled = P.pool != nullptr && P.cbvh_lds_off != ~0u &&\n"
-         "                        !(P.flags & RT_FLAG_REFERENCE_BVH);\n"
-      << "    if (pooled) {\n      const uint4 phd[" << NT << "] = {";
-    for (int j = 0; j < NT; ++j) o << (j ? ", " : "") << "ld4u(N + " << N[pool[j].node + 3] << "u)";
-    o << "};\n      d3 po[" << NT << "], pdr[" << NT << "];\n";
-    for (int j = 0; j < NT; ++j) {
-      // the subtree's frame ray: the world ray through the frame's chain, root first (the same
-      // translate_in / rotate_y_in arithmetic as the sequence below and frame_ray)
-      o << "      {\n        d3 o = ro, d = rd;\n";
-      for (size_t x : pool[j].chain) {
-        if ((N[x] & 0xffu) == RTL_TRANSLATE)
-          o << "        translate_in(" << lit3(pd(N, x, 2), pd(N, x, 3), pd(N, x, 4)) << ", o);\n";
-        else
-          o << "        rotate_y_in(" << lit(pd(N, x, 2)) << ", " << lit(pd(N, x, 3)) << ", o, d);\n";
-      }
-      o << "        po[" << j << "] = o;\n        pdr[" << j << "] = d;\n      }\n";
-    }
-    o << "      cbvh_pool<" << NT << ">(P, phd, po, pdr, tm, tmin, pw, ro, rd);\n"
-         "      o = ro;\n      d = rd;\n    }\n";
-  }
   size_t node = F.hdr.root;
   int frame = -1;
   bool wlen = false;  // |rd| emitted for the world frame's volumes
@@ -538,48 +459,11 @@ std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees)
       node = N[node + 1];
     } else if (ty == RTL_BVH) {
       // BvhNode subtree [node, skip) per lane (rt_kernel.h traverse<UNI> RTL_BVH)
-      const int j = pool_index(node);
       o << "    if (BVH) {\n      double tb;\n      uint32_t bn = 0u;\n      int bf = -1;\n"
         << "      bool sub;\n";
-      if (j >= 0) {
-        // the pooled walk's smallest candidate against the list's interval [tmin, closest]; the
-        // walk's own flag, or a candidate within 3 kTieRel of closest: the reference order decides
-        o << "      if (pooled) {\n"
-          << "        const uint32_t pc = pw.code[" << j << "];\n"
-          << "        tb = pw.t[" << j << "];\n"
-          << "        bn = pc & 0x3fffffffu;\n        bf = " << frame << ";\n"
-          << "        const bool ph = ((pc >> 30) & 1u) != 0u;\n"
-             "        const bool pf = (pc >> 31) != 0u ||\n"
-             "                        (ph && closest < kInf && fabs(tb - closest) <= closest * (3.0 * kTieRel));\n"
-             "        sub = ph && tb < closest;\n"
-             "        if (__ballot(pf) != 0ull && pf)\n"
-          << "          sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, " << N[node + 1]
-          << "u, ro, rd, tm, o, d, " << frame << ", tmin, closest, tb, bn, bf, g, C);\n"
-          << "      } else {\n  ";
-      }
-      const char* seq_env = std::getenv("RT_SEQ_INF");  // diagnostics: the pooled walks' interval
-      const bool seq_inf = seq_env && *seq_env && *seq_env != '0';
-      if (seq_inf && G.bvh) {
-        // (A/B only: a later subtree walked with tmax = +inf and the list's interval applied
-        // afterwards, as the pooled walks do; measures the culling the tmax = +inf walk loses)
-        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, " << N[node + 1]
-          << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
-          << ", tmin, kInf, tb, bn, bf, g, C);\n"
-          << "      {\n        const bool pf = sub && closest < kInf && fabs(tb - closest) <= closest * (3.0 * kTieRel);\n"
-          << "        sub = sub && tb < closest;\n"
-          << "        if (__ballot(pf) != 0ull && pf)\n"
-          << "          sub = traverse<true, COUNT, VOLB, false, BVH>(P, " << node << "u, " << N[node + 1]
-          << "u, ro, rd, tm, o, d, " << frame << ", tmin, closest, tb, bn, bf, g, C);\n      }\n";
-      } else {
-        // a subtree with a column grid (rt_layout.h GRID, RT_GRID=1) instantiates grid_walk
-        const uint32_t ob = N[node + 3];
-        const bool grid = ob != 0u && (size_t)ob + 8 <= N.size() && N[(size_t)ob + 3] > 4u &&
-                          N[(size_t)ob + 4] != 0u;
-        o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH" << (grid ? ", true" : "") << ">(P, "
-          << node << "u, " << N[node + 1] << "u, " << ob << "u, ro, rd, tm, o, d, " << frame
-          << ", tmin, closest, tb, bn, bf, g, C);\n";
-      }
-      if (j >= 0) o << "      }\n";
+      o << "      sub = bvh_subtree<true, COUNT, VOLB, BVH>(P, " << node << "u, " << N[node + 1]
+        << "u, " << N[node + 3] << "u, ro, rd, tm, o, d, " << frame
+        << ", tmin, closest, tb, bn, bf, g, C);\n";
       o << "      closest = sub ? tb : closest;\n      code = sub ? " << kBvhCode << "u : code;\n"
         << "      bhn = sub ? bn : bhn;\n      bhf = sub ? bf : bhf;\n    }\n";
       G.bvh = true;
@@ -986,12 +870,14 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
   };
   bool loaded = load();
   if (!loaded && k.cached) {
-    // a stale, incompatible or damaged cache entry: drop it and compile the source instead of
-    // leaving the scene on the interpreter (a silent slowdown)
+    // a cache entry that does not load (damaged, incompatible, or a transient failure such as
+    // an out-of-memory error): compile the source for this process instead of leaving the scene
+    // on the interpreter (a silent slowdown). The file is left alone: it pins the benchmark
+    // kernels to the build-time compiler, and a transient failure must not
+    // make every later process compile differently.
     const std::string path = log->substr(std::string("code-object cache: ").size());
-    std::fprintf(stderr, "rt_jit: cached code object %s failed to load; recompiling\n",
+    std::fprintf(stderr, "rt_jit: cached code object %s failed to load; recompiling (file kept)\n",
                  path.c_str());
-    std::remove(path.c_str());
     rc = compile(s, arch, &code, log, false);
     if (rc != 0) return rc;
     k.cached = false;

@@ -15,11 +15,7 @@ namespace rtj {
 // time, unrolled, with every record's constants as literals; a BVH subtree record becomes a call
 // of the interpreter's per-lane walker. Empty when the scene has records the generator does not
 // emit or is too large; *why says which.
-// When the top level holds 2 to 4 BVH subtrees with compact ordered BVHs, their walks run as one
-// queue per wave (rt_kernel.h cbvh_pool) and *pool_trees (may be NULL) receives their number (0:
-// no pooled walks). Opt-in, RT_POOL=1 at scene creation: slower at C4. The render then
-// provides TraceParams::pool (rt_device.hip, rt_kernel.h PoolLayout).
-std::string generate(const rtf::FlatScene& F, std::string* why, int* pool_trees = nullptr);
+std::string generate(const rtf::FlatScene& F, std::string* why);
 
 // Template arguments of the path kernel (rt_kernel.h trace_body) the generated walker runs in;
 // the same as the ahead-of-time interpreter kernel the scene would otherwise launch.

@@ -319,8 +319,6 @@ struct TraceParams {
   double* __restrict__ part;
   unsigned long long* __restrict__ ops;
   unsigned int* __restrict__ queue;  // next unclaimed pool (zeroed before each launch)
-  // pooled BVH walks (cbvh_pool): one PoolLayout block per resident wave, or null (not pooled)
-  double* __restrict__ pool;
   int n_pools;    // pools of this launch: n_pairs_r + (pairs - n_pairs_r) * n_blk
   int n_pairs_r;  // (tile, s_j) pairs rendered as row items (one item per pixel, all s_i)
   int n_pairs_a;  // pairs [n_pairs_r, n_pairs_a): segment items; the rest one item per sample
@@ -922,9 +920,7 @@ __device__ __forceinline__ bool volume_hit(const TraceParams& P, uint32_t node, 
 
 // A BVH subtree [node, stop) walked per lane: its ordered BVH when it has one (obvh != 0),
 // otherwise (and always in the op-counting build) the reference tree in the reference order.
-// GRID: the subtree may have a column grid (rt_layout.h GRID, RT_GRID=1 scenes): set by the
-// generated walker for exactly those subtrees, so no other kernel carries grid_walk's code.
-template <bool MAIN, bool COUNT, bool VOLB, bool BVH, bool GRID = false>
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
@@ -1646,408 +1642,7 @@ __device__ __forceinline__ bool cbvh_walk(const TraceParams& P, uint4 hd, d3 o, 
                                                 hit_node, hit_frame, flag);
 }
 
-// ---------------------------------------------------------------- column grid walk
-// A BVH subtree whose leaves each lie in one cell of a regular grid over x and z (rt_layout.h
-// GRID; final_scene's ground: 20 x 20 boxes of random height) is walked by marching the ray
-// through the grid's columns along its major axis instead of stepping the tree: per column the
-// minor cells the ray can be in (1 to 3) and, for each whose leaf top lies above the ray's lowest
-// point in the column, the leaf's exact test (obvh_leaf) with cbvh_walk_t's candidate logic and
-// tie flag. The march is conservative: every position is widened by a margin m (the grid's own
-// tolerance plus 2^-18 of the coordinates' magnitude, far above the f32 roundings), so every cell
-// whose leaf can hold a candidate at t <= closest (1 + 4 kTieRel) is tested, and the columns stop
-// once the next one starts beyond that. The result and flag are therefore cbvh_walk_t's: the same
-// smallest candidate, the same two smallest values of {tmax, candidates} within the tie window.
-template <bool MAIN>
-__device__ bool grid_walk(const TraceParams& P, uint32_t gb, d3 o, d3 d, double tm, int frame,
-                          double tmin, double tmax, double& t_out, uint32_t& hit_node,
-                          int& hit_frame, bool& flag) {
-  const gptr N = (gptr)P.nodes;
-  const kptr G = (kptr)P.nodes + gb;
-  auto gf = [&](int k) { return __uint_as_float(G[k]); };
-  const uint32_t nx = G[0], nz = G[1];
-  const float X0 = gf(4), Z0 = gf(5), Wx = gf(6), Wz = gf(7), iWx = gf(8), iWz = gf(9);
-  const float Ylo = gf(10), Yhi = gf(11), mg = gf(12);
-  typedef uint32_t v2u_t __attribute__((ext_vector_type(2)));
-  typedef const __attribute__((address_space(3))) v2u_t* lc_t;
-  const lc_t cells = (lc_t)(rt_lds + P.cbvh_lds_off + G[2]);  // staged with the compact trees
-  const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
-  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-  const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-  const float m = fmaf(fmaxf(fabsf(ox), fmaxf(fabsf(oy), fabsf(oz))), 0x1p-18f, mg);
-  double closest = tmax, second = kInf;
-  bool hit = false;
-  uint32_t hn = 0;
-  auto cand = [&](bool valid, double t, uint32_t rec) {  // cbvh_walk_t's
-    const double te = valid ? t : kInf;
-    second = fmin(second, fmax(closest, te));
-    const bool win = te < closest;
-    closest = win ? te : closest;
-    hn = win ? rec : hn;
-    hit = hit | win;
-  };
-  // the cut: an f32 bound >= closest (1 + 4 kTieRel)
-  float cut = (float)(closest + closest * 0x1p-20);
-  // the grid's box widened by m: [t0, t1]
-  const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy),
-              idz = __builtin_amdgcn_rcpf(dz);
-  // entry and exit times of [lo, hi] by the sign of 1/d (as the octant's near and far bounds): a
-  // NaN time (0 * inf, the origin on a bound of an axis the ray runs parallel to) stays NaN and
-  // constrains nothing in the fmaxf / fminf below
-  auto slab = [](float lo, float hi, float oo, float id, float& tn, float& tf) {
-    const float a = (lo - oo) * id, b = (hi - oo) * id;
-    const bool neg = id < 0.0f;
-    tn = neg ? b : a;
-    tf = neg ? a : b;
-  };
-  float tnx, tfx, tny, tfy, tnz, tfz;
-  slab(X0 - m, fmaf((float)nx, Wx, X0) + m, ox, idx, tnx, tfx);
-  slab(Ylo - m, Yhi + m, oy, idy, tny, tfy);
-  slab(Z0 - m, fmaf((float)nz, Wz, Z0) + m, oz, idz, tnz, tfz);
-  const float t0 = fmaxf(fmaxf((float)(tmin - fabs(tmin) * 0x1p-20), tnx), fmaxf(tny, tnz));
-  const float t1 = fminf(tfx, fminf(tfy, tfz));
-  // the major axis a (x when the ray crosses columns of x at least as fast as rows of z). One
-  // march with the ray's per-axis values selected per lane: instantiating it per major axis runs
-  // the two instances (and their leaf tests) one after the other in a wave whose lanes differ
-  // (C4 +18.8 %, profiles/r05n_ab_grid_peraxis.log).
-  const bool xa = fabsf(dx) * Wz >= fabsf(dz) * Wx;
-  const float oa = xa ? ox : oz, da = xa ? dx : dz, ida = xa ? idx : idz;
-  const float ob = xa ? oz : ox, db = xa ? dz : dx, idb = xa ? idz : idx;
-  const float A0 = xa ? X0 : Z0, Wa = xa ? Wx : Wz, iWa = xa ? iWx : iWz;
-  const float B0 = xa ? Z0 : X0, Wb = xa ? Wz : Wx, iWb = xa ? iWz : iWx;
-  const int na = (int)(xa ? nx : nz), nb = (int)(xa ? nz : nx);
-  const uint32_t sa = xa ? nz : 1u, sb = xa ? 1u : nz;  // cell = i_x nz + i_z
-  // columns in the order the ray's times of them increase (by the sign of 1/d_a, so a vertical
-  // ray's -0 runs downwards); the first one holds the ray's position at t0 moved back by m
-  const int step = ida < 0.0f ? -1 : 1, jstep = idb < 0.0f ? -1 : 1;
-  const float pa = fmaf(t0, da, oa);
-  int ia = (int)floorf(((step > 0 ? pa - m : pa + m) - A0) * iWa);
-  ia = min(max(ia, 0), na - 1);
-#ifdef RT_PROF
-  uint32_t pf_box = 0, pf_leaf = 0;
-  const unsigned long long pf_t0 = __builtin_readcyclecounter();
-#endif
-  // Per column, in the order the ray reaches them, the minor cells it can be in over the
-  // column's interval [ta, tb]; per cell its own interval (widened by m as the columns) against
-  // the cut, and the ray's lowest y over it against the top of the cell's leaf; then the leaf.
-  // (tend = min(t1, cut): the cut, tightened by the grid's exit. The while-while form of
-  // cbvh_walk_t, leaves of all lanes together after each lane's advance, measured +8.4 % in one
-  // A/B whose log was overwritten.)
-  float tend = fminf(t1, cut);
-  if (t0 <= tend) {
-    for (; ia >= 0 && ia < na; ia += step) {
-      const float lo = fmaf((float)ia, Wa, A0) - m, hi = fmaf((float)(ia + 1), Wa, A0) + m;
-      float tin, tout;
-      slab(lo, hi, oa, ida, tin, tout);
-      const float ta = fmaxf(t0, tin);
-      if (ta > tend) break;  // this column (and every later one) starts past the cut
-      const float tb = fminf(tend, tout);
-#ifdef RT_PROF
-      ++pf_box;
-#endif
-      if (!(ta <= tb)) continue;  // the ray left this column before t0
-      const float pb0 = fmaf(ta, db, ob), pb1 = fmaf(tb, db, ob);
-      const int jb0 = max((int)floorf((fminf(pb0, pb1) - m - B0) * iWb), 0);
-      const int jb1 = min((int)floorf((fmaxf(pb0, pb1) + m - B0) * iWb), nb - 1);
-      for (int k = 0, j = jstep > 0 ? jb0 : jb1; k <= jb1 - jb0; ++k, j += jstep) {
-        float tcin, tcout;
-        slab(fmaf((float)j, Wb, B0) - m, fmaf((float)(j + 1), Wb, B0) + m, ob, idb, tcin, tcout);
-        const float tc = fmaxf(ta, tcin), td = fminf(fminf(tb, tend), tcout);
-        if (!(tc <= td)) continue;
-        const float ylo = fminf(fmaf(tc, dy, oy), fmaf(td, dy, oy)) - m;
-        const v2u_t c = cells[(uint32_t)ia * sa + (uint32_t)j * sb];
-        if (!(ylo <= __uint_as_float(c.x))) continue;
-#ifdef RT_PROF
-        ++pf_leaf;
-#endif
-        const double closest_before = closest;
-        obvh_leaf(N, c.y, o, d, r, tm, tmin, cand);
-        if (closest != closest_before) tend = fminf(tend, (float)(closest + closest * 0x1p-20));
-      }
-    }
-  }
-  flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
-         (hit & (closest <= tmin * (1.0 + kTieRel)));
-#ifdef RT_PROF
-  {
-    const unsigned long long dt = __builtin_readcyclecounter() - pf_t0;
-    uint32_t mb = pf_box, ml = pf_leaf, sbx = pf_box, sl = pf_leaf;
-    for (int k = 32; k > 0; k >>= 1) {
-      mb = max(mb, (uint32_t)__shfl_xor((int)mb, k));
-      ml = max(ml, (uint32_t)__shfl_xor((int)ml, k));
-      sbx += (uint32_t)__shfl_xor((int)sbx, k);
-      sl += (uint32_t)__shfl_xor((int)sl, k);
-    }
-    unsigned long long* pc = P.ops + 40 + (frame < 0 ? 0 : 6);
-    const unsigned long long fl = __popcll(__ballot(flag));
-    if (prof_first_lane()) {
-      atomicAdd(&pc[0], (unsigned long long)sbx);
-      atomicAdd(&pc[2], (unsigned long long)sl);
-      atomicAdd(&pc[1], (unsigned long long)mb);
-      atomicAdd(&pc[3], (unsigned long long)ml);
-      atomicAdd(&pc[4], 1ull);
-      atomicAdd(&pc[5], dt);
-      atomicAdd(&P.ops[52], fl);
-    }
-  }
-#endif
-  if (hit) {
-    t_out = closest;
-    if (MAIN) {
-      hit_node = hn;
-      hit_frame = frame;
-    }
-  }
-  return hit;
-}
-
-// ---------------------------------------------------------------- pooled BVH walks
-// A world query visits every top-level BVH subtree of the list (hittable.rs:88-109 ->
-// BvhNode::hit :216-236), and each walk runs until the wave's slowest lane is done: at C4 the
-// ground-box walk's box steps ran at a SIMD efficiency of 6.0 / 18.3 and the sphere cluster's at
-// 2.0 / 13.5. cbvh_pool walks a wave's NT x 64 trees-by-lanes as ONE queue of
-// tasks (task k: tree k >> 6 of lane k & 63): each lane starts on its own ray's first tree, and
-// lanes that finish early take the next queued task -- another lane's walk of a later tree --
-// once RT_POOL_THR lanes wait (ballot + mbcnt, one setup block for all of them), so a wave runs
-// about max(longest walk, mean work) instead of the sum of its per-tree maxima.
-//
-// Semantics. The queued walks run with tmax = +inf (the list's closest hit before each subtree
-// is not known when the pool starts), so each returns its subtree's smallest candidate t* and
-// record with cbvh_walk_t's arithmetic and tie flag. At the subtree's place in the list the
-// generated walker (rt_jit.cpp) then applies the reference's interval [tmin, closest]: t* wins
-// when t* < closest; the lane re-walks the reference tree in the reference order with the true
-// interval (traverse<LANE>, as bvh_subtree does for flagged lanes) when the walk flagged it or
-// t* lies within 3 kTieRel of closest (where the reference's answer depends on its culling and
-// visiting order: a quad at t = closest is inside Quad::hit's inclusive interval, a sphere's is
-// not, an AABB entering at closest is culled). A walk without random draws (ordered BVHs only
-// hold QUAD / QUADS / SPHERE leaves) may run at any time, so the draw order is unchanged.
-//
-// Exchange. Rays of trees 1.. and every task's result go through the wave's block of
-// TraceParams::pool (global, L2-resident: 4.3 KB per wave and tree): the owner stores its rays
-// before the pool, an executing lane reads one (7 doubles) when it takes the task and stores the
-// result (t, record | hit << 30 | flag << 31); the owner reads its NT results after the pool.
-#ifndef RT_POOL_THR
-#define RT_POOL_THR 16
-#endif
-// One queued task of trees 1..: its ray in f64 (7 rows: o.xyz, d.xyz, time) and the walk's f32
-// slab constants (7 word rows: 1/d.xyz, -o/d.xyz as f32, the octant's bound offsets packed), all
-// formed by the owner with every lane of the wave active, so that a refill only loads them.
-constexpr uint32_t kPoolRayD = 7, kPoolRayW = 7;
-template <int NT>
-struct PoolLayout {  // doubles of one wave's block of TraceParams::pool
-  static constexpr uint32_t rays = 0;                                   // (NT-1) x 7 f64 rows
-  static constexpr uint32_t cst = (NT - 1) * kPoolRayD * 64;            // (NT-1) x 7 u32 rows
-  static constexpr uint32_t saved = cst + (NT - 1) * kPoolRayW * 32;    // the world ray: 6 rows
-  static constexpr uint32_t t = saved + 6 * 64;                         // NT rows of t
-  static constexpr uint32_t code = t + NT * 64;                         // NT u32 rows of codes
-  static constexpr uint32_t doubles = code + NT * 32;
-};
-template <int NT>
-struct PoolOut {
-  double t[NT];
-  uint32_t code[NT];  // record | hit << 30 | flag << 31
-};
-// The caller's world ray (wo, wd) is parked in the block during the walks and read back after
-// them (the same values): the path state the bounce keeps across the walks is then not held in
-// registers while the walk state is (157 -> 168 VGPRs and 19 spilled otherwise).
-template <int NT>
-__device__ __forceinline__ void cbvh_pool(const TraceParams& P, const uint4 (&hd)[NT],
-                                          const d3 (&o)[NT], const d3 (&d)[NT], double tm,
-                                          double tmin, PoolOut<NT>& R, d3& wo, d3& wd) {
-  static_assert(NT >= 2 && NT <= 4, "cbvh_pool: 2 to 4 trees");
-  typedef const __attribute__((address_space(3))) uint8_t* lb_t;
-  typedef __attribute__((address_space(3))) uint8_t* lbw_t;
-  typedef const __attribute__((address_space(3))) uint32_t* lw_t;
-  typedef __attribute__((address_space(3))) uint32_t* ls_t;
-  typedef const __attribute__((address_space(3))) f32x2* lf2_t;
-  typedef PoolLayout<NT> PL;
-  const gptr N = (gptr)P.nodes;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  double* const wb = P.pool + (size_t)wave * PL::doubles;
-  uint32_t* const wcst = reinterpret_cast<uint32_t*>(wb + PL::cst);
-  uint32_t* const wcode = reinterpret_cast<uint32_t*>(wb + PL::code);
-  // a ray's walk constants (cbvh_walk_t's prologue): f32 1/d and -o/d, the octant's offsets
-  struct Cst {
-    float ix, iy, iz, nx, ny, nz;
-    uint32_t oct;  // onx | ony << 8 | onz << 16
-  };
-  auto consts = [](d3 ro_, d3 rd_) {
-    const d3 inv = mk(rcp_w(rd_.x), rcp_w(rd_.y), rcp_w(rd_.z));
-    Cst c;
-    c.ix = (float)inv.x, c.iy = (float)inv.y, c.iz = (float)inv.z;
-    c.nx = -((float)ro_.x * c.ix), c.ny = -((float)ro_.y * c.iy), c.nz = -((float)ro_.z * c.iz);
-    c.oct = (inv.x < 0.0 ? 8u : 0u) | (inv.y < 0.0 ? 24u : 16u) << 8 | (inv.z < 0.0 ? 40u : 32u) << 16;
-    return c;
-  };
-#pragma unroll
-  for (int k = 1; k < NT; ++k) {  // the owner publishes its tasks of trees 1..
-    double* b = wb + PL::rays + (k - 1) * kPoolRayD * 64 + lane;
-    b[0] = o[k].x, b[64] = o[k].y, b[128] = o[k].z;
-    b[192] = d[k].x, b[256] = d[k].y, b[320] = d[k].z, b[384] = tm;
-    const Cst c = consts(o[k], d[k]);
-    uint32_t* w = wcst + (k - 1) * kPoolRayW * 64 + lane;
-    w[0] = __float_as_uint(c.ix), w[64] = __float_as_uint(c.iy), w[128] = __float_as_uint(c.iz);
-    w[192] = __float_as_uint(c.nx), w[256] = __float_as_uint(c.ny), w[320] = __float_as_uint(c.nz);
-    w[384] = c.oct;
-  }
-  {
-    double* sv = wb + PL::saved + lane;
-    sv[0] = wo.x, sv[64] = wo.y, sv[128] = wo.z, sv[192] = wd.x, sv[256] = wd.y, sv[320] = wd.z;
-  }
-  const lbw_t stack_b = (lbw_t)rt_lds + P.stack_lds_off + 4u * threadIdx.x;
-  const uint32_t sstep = 4u * blockDim.x;
-  auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
-  constexpr float kBoxPos = 1.0f + 0x1p-18f;  // tmin >= 0: cbvh_walk_t<TPOS = true>'s box test
-  const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
-  constexpr uint32_t kDone = 0xffffu;
-  // the task in flight (or, on a waiting lane, the last one finished): its ray, walk constants,
-  // tree and walk state
-  uint32_t task = lane;
-  d3 to = o[0], td = d[0], r;
-  double ttm = tm;
-  f32x2 ix2, iy2, iz2, nox2, noy2, noz2;
-  uint32_t onx, ony, onz;
-  lb_t base;
-  lw_t refs, leaves;
-  double closest, second;
-  float close_f;
-  uint32_t hn, ref, sp;
-  bool hit;
-  auto start = [&](Cst c) {  // cbvh_walk_t's prologue from the task's constants
-    const uint32_t tr = task >> 6;
-    uint4 h = hd[0];
-#pragma unroll
-    for (int k = 1; k < NT; ++k) h = tr == (uint32_t)k ? hd[k] : h;
-    const uint32_t n_int = (h.x - 1u) >> 1;
-    base = (lb_t)rt_lds + P.cbvh_lds_off + h.y;
-    refs = reinterpret_cast<lw_t>(base + (size_t)n_int * 48u);
-    leaves = refs + n_int;
-    onx = c.oct & 0xffu, ony = (c.oct >> 8) & 0xffu, onz = c.oct >> 16;
-    r = mk(rcp_nr1(td.x), rcp_nr1(td.y), rcp_nr1(td.z));
-    ix2 = f32x2{c.ix, c.ix}, iy2 = f32x2{c.iy, c.iy}, iz2 = f32x2{c.iz, c.iz};
-    nox2 = f32x2{c.nx, c.nx}, noy2 = f32x2{c.ny, c.ny}, noz2 = f32x2{c.nz, c.nz};
-    closest = kInf;
-    second = kInf;
-    close_f = __builtin_inff();
-    hn = 0u;
-    hit = false;
-    sp = 0u;
-    ref = h.z & 0xffffu;
-  };
-  auto publish = [&]() {  // the finished task's result to its owner's row
-    const bool flag = ((second < kInf) & (second <= closest * (1.0 + 3.0 * kTieRel))) |
-                      (hit & (closest <= tmin * (1.0 + kTieRel)));
-    const uint32_t tr = task >> 6, ow = task & 63u;
-    wb[PL::t + tr * 64u + ow] = closest;
-    wcode[tr * 64u + ow] = hn | (hit ? 1u << 30 : 0u) | (flag ? 1u << 31 : 0u);
-  };
-  auto cand = [&](bool valid, double t, uint32_t rec) {  // cbvh_walk_t's
-    const double te = valid ? t : kInf;
-    second = fmin(second, fmax(closest, te));
-    const bool win = te < closest;
-    closest = win ? te : closest;
-    hn = win ? rec : hn;
-    hit = hit | win;
-  };
-  auto box = [&](float tnx, float tfx, float tny, float tfy, float tnz, float tfz, float& tn) {
-    tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
-    const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
-    return tn <= tf * kBoxPos;
-  };
-  auto entry = [](uint32_t child, float tn) {
-    return child | (tn < 0.0f ? 0xff800000u : (__float_as_uint(tn) & 0xffff0000u));
-  };
-  auto pop = [&]() -> uint32_t {
-    const float cut = close_f * kBoxPos;
-    while (sp > 0) {
-      sp -= sstep;
-      const uint32_t e = *slot(sp);
-      if (!(__uint_as_float(e & 0xffff0000u) > cut)) return e & 0xffffu;
-    }
-    return kDone;
-  };
-  start(consts(to, td));
-  bool busy = true;
-  uint32_t next = 64u;  // wave-uniform: the next unclaimed task
-  constexpr uint32_t kTasks = 64u * NT;
-  // (a guard against a pool that never drains: every iteration tests a leaf or ends a task on
-  // each lane that is not waiting, or hands out tasks, and the pool's NT x 64 tasks visit at most
-  // 2^15 leaves each (rt_layout.h CBVH), so a well-formed pool ends within NT x 2^21 iterations
-  // -- in practice a few dozen; rt_scene_create refuses malformed trees before they reach the
-  // device)
-  for (uint32_t guard = 0; guard < (uint32_t)NT << 21; ++guard) {
-    while (ref < 0x8000u) {  // cbvh_walk_t's step
-      const lb_t nb = base + ref * 48u;
-      const f32x2 NX = *reinterpret_cast<lf2_t>(nb + onx), FX = *reinterpret_cast<lf2_t>(nb + (onx ^ 8u));
-      const f32x2 NY = *reinterpret_cast<lf2_t>(nb + ony), FY = *reinterpret_cast<lf2_t>(nb + (ony ^ 8u));
-      const f32x2 NZ = *reinterpret_cast<lf2_t>(nb + onz), FZ = *reinterpret_cast<lf2_t>(nb + (onz ^ 8u));
-      const uint32_t rr = refs[ref];
-      const f32x2 tnx = __builtin_elementwise_fma(NX, ix2, nox2), tfx = __builtin_elementwise_fma(FX, ix2, nox2);
-      const f32x2 tny = __builtin_elementwise_fma(NY, iy2, noy2), tfy = __builtin_elementwise_fma(FY, iy2, noy2);
-      const f32x2 tnz = __builtin_elementwise_fma(NZ, iz2, noz2), tfz = __builtin_elementwise_fma(FZ, iz2, noz2);
-      float tn0, tn1;
-      const bool h0 = box(tnx.x, tfx.x, tny.x, tfy.x, tnz.x, tfz.x, tn0);
-      const bool h1 = box(tnx.y, tfx.y, tny.y, tfy.y, tnz.y, tfz.y, tn1);
-      const bool first0 = h0 && (!h1 || (tn0 <= tn1));
-      const uint32_t r0 = rr & 0xffffu, r1 = rr >> 16;
-      const bool any = h0 || h1;
-      const uint32_t nref = first0 ? r0 : r1;
-      *slot(sp) = first0 ? entry(r1, tn1) : entry(r0, tn0);
-      sp += (h0 && h1) ? sstep : 0u;
-      ref = any ? nref : pop();
-    }
-    if (ref != kDone) {  // a leaf whose box was hit
-      const double closest_before = closest;
-      obvh_leaf(N, leaves[ref & 0x7fffu], to, td, r, ttm, tmin, cand);
-      if (closest != closest_before) close_f = (float)(closest + closest * (2.0 * kTieRel));
-      ref = pop();
-    }
-    busy = busy && ref != kDone;  // a finished task waits with its result in registers
-    const unsigned long long idle = __ballot(!busy);
-    const unsigned long long work = __ballot(busy);
-    if (next >= kTasks) {
-      if (work == 0ull) break;
-    } else if (__popcll(idle) >= RT_POOL_THR || work == 0ull) {
-      // refill: every waiting lane publishes its last result and takes the next queued task
-      // (its rank among the waiting lanes), the task's ray and constants as the owner made them
-      if (!busy) {
-        publish();
-        const uint32_t k = next + __builtin_amdgcn_mbcnt_hi(
-                                      (uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-        if (k < kTasks) {
-          task = k;
-          const uint32_t row = (k >> 6) - 1u, ow = k & 63u;
-          const double* b = wb + PL::rays + row * kPoolRayD * 64u + ow;
-          const uint32_t* w = wcst + row * kPoolRayW * 64u + ow;
-          to = mk(b[0], b[64], b[128]);
-          td = mk(b[192], b[256], b[320]);
-          ttm = b[384];
-          Cst c;
-          c.ix = __uint_as_float(w[0]), c.iy = __uint_as_float(w[64]), c.iz = __uint_as_float(w[128]);
-          c.nx = __uint_as_float(w[192]), c.ny = __uint_as_float(w[256]), c.nz = __uint_as_float(w[320]);
-          c.oct = w[384];
-          start(c);
-          busy = true;
-        } else {
-          task = 0xffffffffu;  // published; nothing left to take
-        }
-      }
-      next += (uint32_t)__popcll(idle);
-    }
-  }
-  if (task != 0xffffffffu) publish();  // the last task of every lane that still holds one
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-#pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    R.t[k] = wb[PL::t + k * 64u + lane];
-    R.code[k] = wcode[k * 64u + lane];
-  }
-  const double* sv = wb + PL::saved + lane;
-  wo = mk(sv[0], sv[64], sv[128]);
-  wd = mk(sv[192], sv[256], sv[320]);
-}
-
-template <bool MAIN, bool COUNT, bool VOLB, bool BVH, bool GRID>
+template <bool MAIN, bool COUNT, bool VOLB, bool BVH>
 __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, uint32_t obvh,
                             d3 wo, d3 wd, double tm, d3 o, d3 d, int frame, double tmin,
                             double tmax, double& t_out, uint32_t& hit_node, int& hit_frame,
@@ -2072,11 +1667,8 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
     if (obvh != 0u && !(P.flags & RT_FLAG_REFERENCE_BVH)) {
       bool flag = false;
       const uint4 hd = ld4u((gptr)P.nodes + obvh);  // [n_entries][cbvh block][root ref][streams]
-      const uint32_t grid = GRID && hd.w > 4u ? ((gptr)P.nodes)[obvh + 4] : 0u;
       bool h;
-      if (GRID && grid != 0u && P.cbvh_lds_off != ~0u)  // the column grid in LDS
-        h = grid_walk<MAIN>(P, grid, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
-      else if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
+      if (P.cbvh_lds_off != ~0u && hd.y != ~0u)  // the compact copy in LDS
         h = cbvh_walk<MAIN>(P, hd, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame, flag);
       else
         h = obvh_walk<MAIN>(P, obvh, o, d, tm, frame, tmin, tmax, t_out, hit_node, hit_frame,

@@ -85,7 +85,7 @@
  *   obvh: word offset of the subtree's ordered BVH (below), 0 = none (walk the reference tree).
  * OBVH (rt_obvh.cpp), for a BVH subtree whose leaves are QUAD / QUADS / SPHERE records: an SAH
  * BVH2 over the same leaf records, appended after the record region (n_rec_words):
- *   [n_entries][cbvh block][root ref][streams_off = 8][grid][0][0][0]  (word offsets from the header)
+ *   [n_entries][cbvh block][root ref][streams_off = 8][0][0][0][0]  (word offsets from the header)
  *   streams: 8 ray-direction octants (bit a set = d_a < 0, by sign bit) x n_entries x 8 words,
  *   each a threaded pre-order walk with the near child first. Internal entry:
  *   [skip][0][near_x][far_x][near_y][far_y][near_z][far_z] (f32 bounds of the node's box for the
@@ -104,13 +104,6 @@
  *   level of the deepest tree (child reference | bf16 entry time << 16), header cbvh_stack.
  */
 #define RTL_CBVH_STACK 32
-/* GRID (rt_obvh.cpp grid_block; OBVH header word 4 = its word offset, 0 = none): a tree whose
- * leaves each fit one cell of a regular grid over x and z, walked by rt_kernel.h grid_walk
- * instead of a compact tree (header word 1 = 0xffffffff). Header (16 words, after the streams):
- *   [nx][nz][cells: byte offset in the CBVH region][0] f32 [x0][z0][wx][wz][1/wx][1/wz][y_lo][y_hi]
- *   [margin][0][0][0]; the cells, 16-byte aligned in the CBVH region (staged to LDS with the
- *   trees): nx * nz (index i_x nz + i_z) of [f32 top of the leaf's box, rounded up][leaf record
- *   word] (an empty cell: top = -inf, record 0). */
 /* Leaf record words of the OBVH streams and CBVH leaf arrays carry RTL_LEAF_BOX when the record is
  * a QUADS batch of make_box's six sides in its order (rt_obvh.cpp make_box_batch); the record's
  * word offset is the low 31 bits. */

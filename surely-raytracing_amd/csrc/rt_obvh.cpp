@@ -175,85 +175,6 @@ bool collect(const std::vector<uint32_t>& w, uint32_t x, const std::vector<PrimB
   return true;
 }
 
-// The column grid of a tree (rt_layout.h GRID) when every leaf's box fits one cell of a regular
-// grid over x and z, one leaf per cell, at least half the cells filled and at least 16 leaves
-// (final_scene's ground: 20 x 20 make_box boxes, book2 main.rs). The cells' extents may overlap
-// a leaf box by tol = 2^-10 of a cell (the reference's AABB padding); the walk widens every
-// position by m = 2 tol + 2^-16 of the grid's largest coordinate, plus its own ray term.
-// hdr: the 16 header words (word 2, the cells' byte offset in the CBVH region, is set by the
-// caller); cells: 2 words per cell, walked from LDS.
-bool grid_block(const std::vector<Leaf>& L, std::vector<uint32_t>* hdr,
-                std::vector<uint32_t>* cells) {
-  const size_t n = L.size();
-  // opt-in (RT_GRID=1 at scene creation): at C4 the grid walk measured no faster than the
-  // ground's compact tree (-0.15 %, profiles/r05n_ab_grid_optin.log)
-  const char* on = std::getenv("RT_GRID");
-  if (n < 16 || !(on && *on && *on != '0')) return false;
-  double A0[2], W[2];
-  int na[2];
-  for (int g = 0; g < 2; ++g) {
-    const int a = g ? 2 : 0;
-    // the columns from the leaves at least half as wide as the widest (the cell-filling ones):
-    // their distinct starts; every leaf is then checked against the lattice below
-    double wmax = 0.0, lmin = HUGE_VAL, hmax = -HUGE_VAL;
-    for (size_t k = 0; k < n; ++k) {
-      wmax = std::max(wmax, L[k].b.hi[a] - L[k].b.lo[a]);
-      lmin = std::min(lmin, L[k].b.lo[a]);
-      hmax = std::max(hmax, L[k].b.hi[a]);
-    }
-    if (!(wmax > 0.0) || !std::isfinite(lmin) || !std::isfinite(hmax)) return false;
-    std::vector<double> lo;
-    for (size_t k = 0; k < n; ++k)
-      if (L[k].b.hi[a] - L[k].b.lo[a] >= 0.5 * wmax) lo.push_back(L[k].b.lo[a]);
-    std::sort(lo.begin(), lo.end());
-    int cnt = 1;
-    for (size_t k = 1; k < lo.size(); ++k) cnt += lo[k] - lo[k - 1] > 0.5 * wmax;
-    A0[g] = lmin;
-    na[g] = cnt;
-    W[g] = (hmax - lmin) / cnt;
-    if (cnt < 2 || cnt > 1024 || !(W[g] > 0.0)) return false;
-  }
-  if ((size_t)na[0] * na[1] > 65536 || 2 * n < (size_t)na[0] * na[1]) return false;
-  const double tol = 0x1p-10 * std::min(W[0], W[1]);
-  std::vector<int> cell((size_t)na[0] * na[1], -1);
-  double ylo = HUGE_VAL, yhi = -HUGE_VAL, big = 0.0;
-  for (size_t k = 0; k < n; ++k) {
-    int ij[2];
-    for (int g = 0; g < 2; ++g) {
-      const int a = g ? 2 : 0;
-      const int i = (int)std::floor((L[k].c[a] - A0[g]) / W[g]);
-      if (i < 0 || i >= na[g] || L[k].b.lo[a] < A0[g] + i * W[g] - tol ||
-          L[k].b.hi[a] > A0[g] + (i + 1) * W[g] + tol)
-        return false;
-      ij[g] = i;
-    }
-    int& c = cell[(size_t)ij[0] * na[1] + ij[1]];
-    if (c >= 0) return false;
-    c = (int)k;
-    ylo = std::min(ylo, L[k].b.lo[1]);
-    yhi = std::max(yhi, L[k].b.hi[1]);
-  }
-  if (!std::isfinite(ylo) || !std::isfinite(yhi)) return false;
-  for (int g = 0; g < 2; ++g)
-    big = std::max(big, std::max(std::fabs(A0[g]), std::fabs(A0[g] + na[g] * W[g])));
-  big = std::max(big, std::max(std::fabs(ylo), std::fabs(yhi)));
-  hdr->assign(16, 0u);
-  cells->assign(2 * cell.size(), 0u);
-  uint32_t* B = hdr->data();
-  B[0] = (uint32_t)na[0];
-  B[1] = (uint32_t)na[1];
-  const float f[9] = {(float)A0[0], (float)A0[1], (float)W[0], (float)W[1], (float)(1.0 / W[0]),
-                      (float)(1.0 / W[1]), f32_down(ylo), f32_up(yhi),
-                      f32_up(2.0 * tol + 0x1p-16 * big)};
-  std::memcpy(B + 4, f, sizeof(f));
-  for (size_t c = 0; c < cell.size(); ++c) {
-    const float top = cell[c] < 0 ? -HUGE_VALF : f32_up(L[cell[c]].b.hi[1]);
-    std::memcpy(&(*cells)[2 * c], &top, 4);
-    (*cells)[2 * c + 1] = cell[c] < 0 ? 0u : L[cell[c]].rec;
-  }
-  return true;
-}
-
 }  // namespace
 
 // Outward-rounded f32 bounds of a node's box (the padded f64 box grown by 2^-18 (1 + |coord|)):
@@ -394,25 +315,13 @@ void build_ordered_bvhs(std::vector<uint32_t>& w, uint32_t rec_words,
       em.run(0);
     }
     w[root + 3] = hdr;  // the reference BVH record points at its ordered tree
-    // a column grid replaces the compact tree: its header after the streams (read with scalar
-    // loads), its cells in the CBVH region (staged to LDS with the trees)
-    std::vector<uint32_t> ghdr, gcells;
-    const bool grid = grid_block(leaves, &ghdr, &gcells);
-    if (grid) {
-      while (w.size() % 4) w.push_back(0u);
-      ghdr[2] = (uint32_t)(cbvh.size() * 4);
-      w[hdr + 4] = (uint32_t)w.size();
-      w.insert(w.end(), ghdr.begin(), ghdr.end());
-      cbvh.insert(cbvh.end(), gcells.begin(), gcells.end());
-      while (cbvh.size() % 4) cbvh.push_back(0u);
-    }
     std::vector<uint32_t> blk;
     uint32_t root_ref = 0u;
     w[hdr + 1] = 0xffffffffu;
     // the two-wide compact tree (a 4-wide form walked in about half the steps but tested more
     // boxes and sorted them: 3.3 % slower at C4, profiles/r03_ab_bvh4_vs_bvh2_c4.log; removed)
     int depth = 0;
-    if (!grid && !std::getenv("RT_NO_CBVH") &&
+    if (!std::getenv("RT_NO_CBVH") &&
         compact_tree(B.nodes, leaves, &blk, &root_ref, &depth)) {
       w[hdr + 1] = (uint32_t)(cbvh.size() * 4);  // byte offset in the region
       w[hdr + 2] = root_ref;
@@ -465,8 +374,13 @@ void emulate_walk(const CTree& T, const double o[3], const double d[3], double t
   auto fail = [&](const char* what) {
     if (W.errors++ == 0) W.first_error = what;
   };
-  const double inv[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
-  const bool nx = inv[0] < 0.0, ny = inv[1] < 0.0, nz = inv[2] < 0.0;
+  // the device's slab reciprocals (rt_kernel.h cbvh_walk_t): f32(rcp_nr1(d_a)), within an ulp of
+  // 1/d_a, and NaN for d_a = +-0 (rcp_nr1's 0 * inf; a NaN slab time constrains nothing); the
+  // octant from d's sign bit
+  const double qnan = std::nan("");
+  const double inv[3] = {d[0] == 0.0 ? qnan : 1.0 / d[0], d[1] == 0.0 ? qnan : 1.0 / d[1],
+                         d[2] == 0.0 ? qnan : 1.0 / d[2]};
+  const bool nx = std::signbit(d[0]), ny = std::signbit(d[1]), nz = std::signbit(d[2]);
   const float ix = (float)inv[0], iy = (float)inv[1], iz = (float)inv[2];
   const float ox = (float)o[0], oy = (float)o[1], oz = (float)o[2];
   const float nox = -(ox * ix), noy = -(oy * iy), noz = -(oz * iz);
@@ -547,101 +461,6 @@ void emulate_walk(const CTree& T, const double o[3], const double d[3], double t
   fail("walk did not end");
 }
 
-// rt_kernel.h grid_walk's march over one grid for one ray with no closest hit (the cut at
-// +inf), in the device's f32 arithmetic (1 / d exact here, a 1-ulp reciprocal there): the cells
-// whose leaf the walk would test. G: the grid's 16 header words; cells: its cell words.
-void emulate_grid(const uint32_t* G, const uint32_t* cells, const double o[3], const double d[3],
-                  double tmin, std::vector<uint8_t>& visit) {
-  auto gf = [&](int k) {
-    float f;
-    std::memcpy(&f, &G[k], 4);
-    return f;
-  };
-  const int nx = (int)G[0], nz = (int)G[1];
-  const float X0 = gf(4), Z0 = gf(5), Wx = gf(6), Wz = gf(7), iWx = gf(8), iWz = gf(9);
-  const float Ylo = gf(10), Yhi = gf(11), mg = gf(12);
-  const float ox = (float)o[0], oy = (float)o[1], oz = (float)o[2];
-  const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
-  const float m =
-      std::fmaf(std::fmax(std::fabs(ox), std::fmax(std::fabs(oy), std::fabs(oz))), 0x1p-18f, mg);
-  const float idx = 1.0f / dx, idy = 1.0f / dy, idz = 1.0f / dz;
-  auto slab = [](float lo, float hi, float oo, float id, float& tn, float& tf) {
-    const float a = (lo - oo) * id, b = (hi - oo) * id;
-    tn = id < 0.0f ? b : a;
-    tf = id < 0.0f ? a : b;
-  };
-  // fmaxf / fminf as the device's: a NaN operand is dropped
-  auto fmx = [](float a, float b) { return std::isnan(a) ? b : std::isnan(b) ? a : std::max(a, b); };
-  auto fmn = [](float a, float b) { return std::isnan(a) ? b : std::isnan(b) ? a : std::min(a, b); };
-  float tnx, tfx, tny, tfy, tnz, tfz;
-  slab(X0 - m, std::fmaf((float)nx, Wx, X0) + m, ox, idx, tnx, tfx);
-  slab(Ylo - m, Yhi + m, oy, idy, tny, tfy);
-  slab(Z0 - m, std::fmaf((float)nz, Wz, Z0) + m, oz, idz, tnz, tfz);
-  const float t0 = fmx(fmx((float)(tmin - std::fabs(tmin) * 0x1p-20), tnx), fmx(tny, tnz));
-  const float t1 = fmn(tfx, fmn(tfy, tfz));
-  const bool xa = std::fabs(dx) * Wz >= std::fabs(dz) * Wx;
-  const float oa = xa ? ox : oz, ida = xa ? idx : idz, ob = xa ? oz : ox, db = xa ? dz : dx;
-  const float idb = xa ? idz : idx, A0 = xa ? X0 : Z0, Wa = xa ? Wx : Wz, iWa = xa ? iWx : iWz;
-  const float B0 = xa ? Z0 : X0, Wb = xa ? Wz : Wx, iWb = xa ? iWz : iWx;
-  const int na = xa ? nx : nz, nb = xa ? nz : nx;
-  const float pa = std::fmaf(t0, xa ? dx : dz, oa);
-  int ia = (int)std::floor(((ida >= 0.0f ? pa - m : pa + m) - A0) * iWa);
-  ia = std::min(std::max(ia, 0), na - 1);
-  const int step = ida < 0.0f ? -1 : 1, jstep = idb < 0.0f ? -1 : 1;
-  const float tend = t1;
-  if (!(t0 <= tend)) return;
-  for (; ia >= 0 && ia < na; ia += step) {
-    float tin, tout;
-    slab(std::fmaf((float)ia, Wa, A0) - m, std::fmaf((float)(ia + 1), Wa, A0) + m, oa, ida, tin, tout);
-    const float ta = fmx(t0, tin);
-    if (ta > tend) return;
-    const float tb = fmn(tend, tout);
-    if (!(ta <= tb)) continue;
-    const float pb0 = std::fmaf(ta, db, ob), pb1 = std::fmaf(tb, db, ob);
-    const int jb0 = std::max((int)std::floor((fmn(pb0, pb1) - m - B0) * iWb), 0);
-    const int jb1 = std::min((int)std::floor((fmx(pb0, pb1) + m - B0) * iWb), nb - 1);
-    for (int k = 0, j = jstep > 0 ? jb0 : jb1; k < jb1 - jb0 + 1; ++k, j += jstep) {
-      float tcin, tcout;
-      slab(std::fmaf((float)j, Wb, B0) - m, std::fmaf((float)(j + 1), Wb, B0) + m, ob, idb, tcin, tcout);
-      const float tc = fmx(ta, tcin), td = fmn(fmn(tb, tend), tcout);
-      if (!(tc <= td)) continue;
-      const float ylo = fmn(std::fmaf(tc, dy, oy), std::fmaf(td, dy, oy)) - m;
-      const size_t c = xa ? (size_t)ia * nz + j : (size_t)j * nz + ia;
-      float top;
-      std::memcpy(&top, &cells[2 * c], 4);
-      if (ylo <= top) visit[c] = 1;
-    }
-  }
-}
-
-// The f64 bounds of a grid cell's leaf from its record (rt_layout.h): a make_box batch's six side
-// planes, a sphere's centre +- radius (both centres of a moving one); false for other records.
-bool leaf_bounds(const std::vector<uint32_t>& w, uint32_t rec, double lo[3], double hi[3]) {
-  auto dbl = [&](size_t k) {
-    double v;
-    const uint64_t b = (uint64_t)w[k] | (uint64_t)w[k + 1] << 32;
-    std::memcpy(&v, &b, 8);
-    return v;
-  };
-  const bool box = (rec & RTL_LEAF_BOX) != 0u;
-  rec &= ~RTL_LEAF_BOX;
-  if (box) {  // sides 0 z = max, 1 x = max, 2 z = min, 3 x = min, 4 y = max, 5 y = min
-    auto q = [&](int f) { return dbl((size_t)rec + 4 + (size_t)f * RTL_QUAD_WORDS + 4); };
-    lo[0] = q(3), hi[0] = q(1), lo[1] = q(5), hi[1] = q(4), lo[2] = q(2), hi[2] = q(0);
-    return true;
-  }
-  if ((w[rec] & 0xffu) == RTL_SPHERE) {
-    const double r = std::fabs(dbl(rec + 4 + 6));
-    for (int a = 0; a < 3; ++a) {
-      const double c = dbl(rec + 4 + 2 * a);
-      const double c1 = (w[rec] & RTL_SPHERE_MOVING) ? c + dbl(rec + 4 + 8 + 2 * a) : c;
-      lo[a] = std::min(c, c1) - r, hi[a] = std::max(c, c1) + r;
-    }
-    return true;
-  }
-  return false;
-}
-
 }  // namespace
 
 WalkCheck check_compact_trees(const std::vector<uint32_t>& w, const rtl_scene_header& hdr,
@@ -661,113 +480,6 @@ WalkCheck check_compact_trees(const std::vector<uint32_t>& w, const rtl_scene_he
     return end != 0 && end <= hdr.n_rec_words;
   };
   uint64_t rng = seed ^ 0x5851F42D4C957F2Dull;
-  // the column grids (rt_kernel.h grid_walk): dimensions, block bounds, every filled cell's record
-  for (size_t p = 0; p < hdr.n_rec_words; p += record_words(w[p])) {
-    if ((w[p] & 0xffu) != RTL_BVH || w[p + 3] == 0u) continue;
-    const uint32_t ob = w[p + 3];
-    if ((size_t)ob + 8 > w.size() || w[ob + 3] <= 4u || w[ob + 4] == 0u) continue;
-    const size_t gb = w[ob + 4];
-    ++W.grids;
-    if (gb % 4 != 0 || gb + 16 > w.size()) {
-      fail("column grid header outside the node array");
-      continue;
-    }
-    const uint32_t nx = w[gb], nz = w[gb + 1], off = w[gb + 2];
-    const size_t region0 = hdr.cbvh_word0;
-    if (nx < 1 || nx > 1024 || nz < 1 || nz > 1024 || off % 16 != 0 || hdr.cbvh_words == 0 ||
-        region0 + hdr.cbvh_words > w.size() ||
-        (size_t)off + 8ull * nx * nz > (size_t)hdr.cbvh_words * 4u) {
-      fail("column grid dimensions or cells outside the CBVH region");
-      continue;
-    }
-    const uint32_t* cells = w.data() + region0 + off / 4;
-    bool cells_ok = true;
-    for (size_t c = 0; c < (size_t)nx * nz && cells_ok; ++c) {
-      float top;
-      std::memcpy(&top, &cells[2 * c], 4);
-      if (top != -HUGE_VALF && !leaf_ok(cells[2 * c + 1])) {
-        fail("column grid cell record is not a QUAD / QUADS / SPHERE record inside the record region");
-        cells_ok = false;
-      }
-    }
-    if (!cells_ok || n_rays == 0) continue;
-    // The march is conservative: over random rays (origins inside, outside and on the lattice's
-    // planes and the leaves' tops; random, axis-parallel, vertical and grazing directions), every
-    // filled cell whose leaf box (widened by 2^-40 of the coordinates, the candidates' rounding)
-    // the ray meets at t >= t_min (f64 slab test) is among the cells the march tests.
-    std::vector<std::array<double, 6>> lb((size_t)nx * nz);
-    std::vector<uint8_t> has((size_t)nx * nz, 0);
-    double ext = 0.0;
-    for (size_t c = 0; c < lb.size(); ++c) {
-      float top;
-      std::memcpy(&top, &cells[2 * c], 4);
-      if (top == -HUGE_VALF) continue;
-      double lo[3], hi[3];
-      if (!leaf_bounds(w, cells[2 * c + 1], lo, hi)) continue;
-      has[c] = 1;
-      for (int a = 0; a < 3; ++a) {
-        lb[c][a] = lo[a], lb[c][3 + a] = hi[a];
-        ext = std::max(ext, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
-      }
-    }
-    float gfl[8];
-    std::memcpy(gfl, &w[gb + 4], sizeof(gfl));
-    const double X0 = gfl[0], Z0 = gfl[1], Wx = gfl[2], Wz = gfl[3], Ylo = gfl[6], Yhi = gfl[7];
-    const double e = 0x1p-40 * (ext + 1.0);
-    std::vector<uint8_t> visit(lb.size());
-    for (uint32_t k = 0; k < n_rays; ++k) {
-      double o[3], d[3];
-      const int kind = (int)(splitmix(rng) % 4);
-      const double sx = nx * Wx, sz = nz * Wz, sy = Yhi - Ylo;
-      o[0] = X0 + (u01(rng) * 1.4 - 0.2) * sx;
-      o[1] = Ylo + (u01(rng) * 2.0 - 0.5) * sy;
-      o[2] = Z0 + (u01(rng) * 1.4 - 0.2) * sz;
-      if (kind == 1) {  // on a lattice plane (x and / or z), at a leaf's top
-        const int i = (int)(splitmix(rng) % (nx + 1)), j = (int)(splitmix(rng) % (nz + 1));
-        if (splitmix(rng) & 1) o[0] = X0 + i * Wx;
-        if (splitmix(rng) & 1) o[2] = Z0 + j * Wz;
-        const size_t c = splitmix(rng) % lb.size();
-        if (has[c]) o[1] = lb[c][4];
-      } else if (kind == 2) {  // far outside
-        for (int a = 0; a < 3; ++a) o[a] += (u01(rng) - 0.5) * 8.0 * (sx + sz);
-      }
-      const double z = 2.0 * u01(rng) - 1.0, ph = 6.283185307179586 * u01(rng);
-      const double s = std::sqrt(std::max(0.0, 1.0 - z * z));
-      d[0] = s * std::cos(ph), d[1] = z, d[2] = s * std::sin(ph);
-      const uint64_t sp = splitmix(rng) % 8;
-      if (sp == 0) d[1] *= 1e-7;                                   // grazing
-      if (sp == 1) d[0] = (splitmix(rng) & 1) ? 0.0 : -0.0;        // parallel to the x planes
-      if (sp == 2) d[2] = (splitmix(rng) & 1) ? 0.0 : -0.0;        // parallel to the z planes
-      if (sp == 3) d[0] = d[2] = (splitmix(rng) & 1) ? 0.0 : -0.0;  // vertical
-      if (!(d[0] != 0.0 || d[1] != 0.0 || d[2] != 0.0)) d[1] = -1.0;
-      if (kind == 2) {  // aim the far rays at the grid
-        const double tx = X0 + u01(rng) * sx, ty = Ylo + u01(rng) * sy, tz = Z0 + u01(rng) * sz;
-        d[0] = tx - o[0], d[1] = ty - o[1], d[2] = tz - o[2];
-      }
-      std::fill(visit.begin(), visit.end(), 0);
-      const double tmin = 1e-4;
-      emulate_grid(&w[gb], cells, o, d, tmin, visit);
-      for (size_t c = 0; c < lb.size(); ++c) {
-        if (!has[c] || visit[c]) continue;
-        double t0 = tmin, t1 = HUGE_VAL;
-        for (int a = 0; a < 3 && t0 <= t1; ++a) {
-          const double l = lb[c][a] - e, h = lb[c][3 + a] + e;
-          if (d[a] == 0.0) {
-            if (o[a] < l || o[a] > h) t1 = -1.0;
-            continue;
-          }
-          const double ta = (l - o[a]) / d[a], tb = (h - o[a]) / d[a];
-          t0 = std::max(t0, std::min(ta, tb));
-          t1 = std::min(t1, std::max(ta, tb));
-        }
-        if (t0 <= t1) {
-          fail("column grid march skipped a cell whose leaf the ray meets");
-          break;
-        }
-      }
-      ++W.rays;
-    }
-  }
   if (hdr.cbvh_words == 0) return W;
   const size_t region0 = hdr.cbvh_word0, region_bytes = (size_t)hdr.cbvh_words * 4u;
   if (region0 % 4 != 0 || region0 + hdr.cbvh_words > w.size()) {

@@ -503,7 +503,7 @@ LAYOUT_STATS = ["node_words", "bvh_words", "bvh_records", "dup_records", "volume
 # rt_scene_lds_check (include/rt_mi355x.h RT_LDS_CHECK)
 LDS_CHECK = ["block", "static_lds", "stage_bytes", "cbvh_lds_off", "cbvh_bytes", "stack_lds_off",
              "cbvh_stack", "lds_bytes", "lds_total", "lds_cu", "trees", "max_depth", "errors",
-             "max_store_slot", "max_live", "rays", "steps", "max_read", "row_lds_off", "grids"]
+             "max_store_slot", "max_live", "rays", "steps", "max_read", "row_lds_off"]
 
 
 def render_multi(blob: "Blob", cam: RtCamera, opts: RtRenderOpts, devices,

@@ -6,6 +6,8 @@ pixel and channel. Both compute the path in f64 with the same per-sample RNG str
 uses fma and ocml while the oracle uses the reference's plain operation order and libm, so
 path decisions agree (identical op counts are asserted) and sums differ only by rounding.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -246,6 +248,38 @@ def _jit_state(blob, cam):
         return ds.jit_info()
     finally:
         ds.close()
+
+
+def test_damaged_cached_code_object_is_recompiled_and_kept(gpu_available, tmp_path):
+    """A cached code object that fails to load (damaged here; in the field also a transient load
+    failure) is recompiled for this process only: the scene still runs its scene-specialised
+    kernel, and the cache file is left in place (deleting it made every later process
+    compile with another compiler). Each render runs in its own process, since the module cache
+    keeps a loaded kernel for the process."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    pkg = str(Path(__file__).resolve().parent.parent / "surely-raytracing_amd")
+    code = ("import sys; sys.path.insert(0, %r); import surely_rt as rt; "
+            "blob, cam = rt.preset_blob('cornell_box', width=16, spp=1); "
+            "ds = rt.DeviceScene(blob); ds.render(cam, rt.make_opts(cam)); "
+            "print('JIT', ds.jit_info()[0]); ds.close()") % pkg
+    env = dict(os.environ, RT_JIT_CACHE_DIR=str(tmp_path), RT_JIT_CACHE_WRITE="1")
+    env.pop("RT_JIT_OPTS", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "JIT 1" in r.stdout, r.stderr[-2000:]
+    files = sorted(tmp_path.glob("*.co"))
+    assert len(files) == 1
+    junk = b"not a code object" * 64
+    files[0].write_bytes(junk)
+    env.pop("RT_JIT_CACHE_WRITE")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "JIT 1" in r.stdout, r.stderr[-2000:]
+    assert "failed to load; recompiling (file kept)" in r.stderr
+    assert files[0].exists() and files[0].read_bytes() == junk
 
 
 def test_jit_kernel_runs_for_cornell(gpu_available):

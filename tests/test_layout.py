@@ -78,22 +78,12 @@ def test_compact_bvhs_fit_the_lds_budget():
     cbvh_walk reads from LDS (48-byte two-child nodes, u16 references), and with the per-lane
     stacks of a 768-thread workgroup (one u32 per tree level: final_scene's trees are 10 and 12
     levels deep, so at most 16 x 4 bytes), the f64 sample sums and the Perlin table it fits the
-    CU's 160 KiB. With RT_GRID=1 (opt-in, rt_layout.h GRID) the ground's 20 x 20 boxes are a
-    column grid instead, its 8-byte cells in the same region."""
-    import os
-
+    CU's 160 KiB."""
     blob, cam = rt.preset_blob("final_scene", width=32, spp=4)
     st2 = rt.layout_stats(blob)
     assert st2["compact_bvhs"] == st2["ordered_bvhs"] == 2
     n_leaves = 400 + 1000
     n_int = n_leaves - 2
     assert n_int * 52 + n_leaves * 4 <= st2["compact_bvh_bytes"] <= n_int * 52 + n_leaves * 4 + 32
-    os.environ["RT_GRID"] = "1"
-    try:
-        st = rt.layout_stats(blob)
-    finally:
-        del os.environ["RT_GRID"]
-    assert st["ordered_bvhs"] == 2 and st["compact_bvhs"] == 1
-    assert 999 * 52 + 1000 * 4 + 400 * 8 <= st["compact_bvh_bytes"] <= 999 * 52 + 1000 * 4 + 400 * 8 + 32
     stacks, sums, perlin = 16 * 768 * 4, 768 * 24, 8960
     assert st2["compact_bvh_bytes"] + stacks + sums + perlin + 512 <= 160 * 1024

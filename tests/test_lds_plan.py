@@ -29,7 +29,10 @@ def _assert_walk_invariants(chk, label):
     assert 4 * chk["max_depth"] <= chk["cbvh_stack"], (label, chk)
     assert chk["rays"] > 0 and chk["steps"] > 0, (label, chk)
     assert chk["max_store_slot"] < chk["max_depth"], (label, chk)
-    assert chk["max_live"] <= chk["max_depth"] - 1, (label, chk)
+    # pending entries: at most k - 1 before the step at an internal node of depth k, k after it
+    # (both children of the deepest node hit: reached by rays parallel to a slab plane, whose NaN
+    # slab times keep every box on that axis, as the device's)
+    assert chk["max_live"] <= chk["max_depth"], (label, chk)
     assert chk["max_read"] <= chk["cbvh_bytes"], (label, chk)
     if chk["cbvh_lds_off"] != 0xFFFFFFFF:  # trees and stacks in LDS: the regions fit the request
         assert chk["cbvh_lds_off"] == chk["stage_bytes"]
@@ -54,7 +57,7 @@ def test_final_scene_at_benchmark_size_stages_its_trees():
     blob, _ = rt.preset_blob("final_scene", width=800, spp=5000, depth=40)
     chk = rt.lds_check(blob, n_rays=20000)
     _assert_walk_invariants(chk, "final_scene")
-    assert chk["trees"] == 2 and chk["grids"] == 0 and chk["block"] == 768
+    assert chk["trees"] == 2 and chk["block"] == 768
     assert chk["cbvh_lds_off"] != 0xFFFFFFFF
     # ... and the row totals of its row items (one f64 value per (pixel, s_j): VERDICT r4 item 4)
     assert chk["row_lds_off"] != 0xFFFFFFFF
@@ -74,29 +77,11 @@ def test_dense_bvh_fuzz_scenes_lds_plan_and_walk(seed):
     _assert_walk_invariants(chk, f"fuzz{seed}")
 
 
-def test_column_grids_are_found_and_checked():
-    """With RT_GRID=1 (opt-in, rt_layout.h GRID) final_scene's ground (20 x 20 boxes) and both
-    grids of the column-grid fuzz scenes get a column grid; its cells' records pass the structural
-    check, and the host restatement of the march (rt_obvh.cpp emulate_grid, the device's f32
-    arithmetic) tests, over random rays -- origins inside, outside and on the lattice's planes and
-    the leaves' tops; random, axis-parallel, vertical and grazing directions -- every cell whose
-    leaf box the ray meets (f64 slab test): the march's margins are conservative. (With the margin
-    set to zero the same check fails thousands of rays per scene.) Without RT_GRID, and for the
-    scenes without such a tree, there is none."""
-    import os
-
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_lattice_bvh_scenes_lds_plan_and_walk(seed):
     from test_bvh_fuzz_gpu import column_grid_scene
 
-    blob, _ = rt.preset_blob("final_scene", width=64, spp=4)
-    assert rt.lds_check(blob, n_rays=0)["grids"] == 0
-    os.environ["RT_GRID"] = "1"
-    try:
-        chk = rt.lds_check(blob, n_rays=20000)
-        assert chk["grids"] == 1 and chk["trees"] == 1 and chk["errors"] == 0, chk
-        for seed in range(1, 7):
-            chk = rt.lds_check(column_grid_scene(seed)[0], n_rays=4000, seed=seed)
-            assert chk["grids"] == 2 and chk["errors"] == 0, (seed, chk)
-        for name in ("cornell_box", "random_balls", "quads"):
-            assert rt.lds_check(rt.preset_blob(name, width=64, spp=4)[0], n_rays=0)["grids"] == 0
-    finally:
-        del os.environ["RT_GRID"]
+    blob, _ = column_grid_scene(seed)
+    chk = rt.lds_check(blob, n_rays=4096, seed=seed)
+    assert chk["trees"] >= 2
+    _assert_walk_invariants(chk, f"lattice{seed}")
