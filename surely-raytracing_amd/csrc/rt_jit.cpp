@@ -288,12 +288,12 @@ bool gen_light_entry(const rtf::FlatScene& F, size_t i, int nest, int sphere0, i
     }
     const uint32_t n = L[off] >> 8, first = L[off + 1];
     const std::string acc = "lsum" + std::to_string(uid++);
-    o << "    {\n    double " << acc << " = 0.0;\n";
+    o << "    {\n    wt " << acc << " = 0;\n";
     for (uint32_t k = 0; k < n; ++k) {
       if (!gen_light_entry(F, first + k, nest - 1, sphere0, uid, o, why)) return false;
       o << "    " << acc << (k == 0 ? " = pv;\n" : " = " + acc + " + pv;\n");
     }
-    o << "    pv = " << acc << " * " << lit(pd(L, off, 0)) << ";\n    }\n";
+    o << "    pv = " << acc << " * (wt)" << lit(pd(L, off, 0)) << ";\n    }\n";
   } else if (type == RTL_QUAD) {
     o << "    {\n      C.inc(RT_OP_LIGHT_PDF_QUAD);\n      double t = 0.0;\n      bool hq;\n";
     const uint32_t axis = RTL_QUAD_AXIS(L[off]);
@@ -310,13 +310,9 @@ bool gen_light_entry(const rtf::FlatScene& F, size_t i, int nest, int sphere0, i
       o << "      hq = quad_test<COUNT>((kptr)P.lights + " << off
         << "u, origin, dir, 0.001, kInf, t, C);\n";
     }
-    o << "      const double len2 = dot(dir, dir);\n"
-         "      const double dist2 = (t * t) * len2;\n"
-         "      const double cosine = fabs(dot(dir, "
-      << lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2))
-      << ")) * rsq_nr(len2);\n"
-         "      const double q = dist2 * rcp_w(cosine * "
-      << lit(pd(L, off, 7)) << ");\n      pv = hq ? q : 0.0;\n    }\n";
+    o << "      const wt q = quad_light_w(dir, t, "
+      << lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2)) << ", " << lit(pd(L, off, 7))
+      << ");\n      pv = hq ? q : (wt)0;\n    }\n";
   } else if (type == RTL_SPHERE) {
     const std::string c = lit3(pd(L, off, 0), pd(L, off, 1), pd(L, off, 2));
     const std::string r = lit(pd(L, off, 3));
@@ -339,8 +335,7 @@ bool gen_light_entry(const rtf::FlatScene& F, size_t i, int nest, int sphere0, i
       o << "      if (hs) {\n        d3 cmo = " << c << " - origin;\n        double r = " << r
         << ";\n        cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));\n      }\n";
     }
-    o << "      const double solid = 2.0 * kPi * (1.0 - cos_max);\n"
-         "      const double q = rcp_w(solid);\n      pv = hs ? q : 0.0;\n    }\n";
+    o << "      const wt q = sphere_light_w(cos_max);\n      pv = hs ? q : (wt)0;\n    }\n";
   }
   return true;
 }
@@ -348,10 +343,10 @@ bool gen_light_entry(const rtf::FlatScene& F, size_t i, int nest, int sphere0, i
 bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string* why) {
   const std::vector<uint32_t>& L = F.lights;
   o << "  template <bool COUNT>\n"
-       "  static __device__ __forceinline__ double lights_pdf(const TraceParams& P, d3 origin, d3 dir,\n"
+       "  static __device__ __forceinline__ wt lights_pdf(const TraceParams& P, d3 origin, d3 dir,\n"
        "      double cos_sl0, Ctr<COUNT>& C) {\n"
        "    (void)P; (void)origin; (void)dir; (void)cos_sl0;\n"
-       "    double sum = 0.0, pv = 0.0;\n";
+       "    wt sum = 0, pv = 0;\n";
   int sphere0 = -1;  // rt_device.hip sphere_light0: the first sphere light
   for (size_t i = 0; i < F.light_offs.size(); ++i)
     if ((L[F.light_offs[i]] & 0xffu) == RTL_SPHERE) {
@@ -369,7 +364,7 @@ bool gen_lights_pdf(const rtf::FlatScene& F, std::ostringstream& o, std::string*
     o << (i == 0 ? "    sum = pv;\n" : "    sum = sum + pv;\n");
   }
   if (F.hdr.lights_is_list && n) {
-    o << "    return sum * " << lit(1.0 / (double)n) << ";\n  }\n";
+    o << "    return sum * (wt)" << lit(1.0 / (double)n) << ";\n  }\n";
   } else {
     o << "    return sum;\n  }\n";
   }
@@ -865,8 +860,12 @@ int get_kernel(const std::string& walker, int device, const Flags& f, Kernel* ou
     if (k.mod) (void)hipModuleUnload(k.mod);
     k.mod = nullptr;
     k.fn = nullptr;
-    return hipModuleLoadData(&k.mod, code.data()) == hipSuccess &&
-           hipModuleGetFunction(&k.fn, k.mod, "rt_trace_jit") == hipSuccess;
+    const bool ok = hipModuleLoadData(&k.mod, code.data()) == hipSuccess &&
+                    hipModuleGetFunction(&k.fn, k.mod, "rt_trace_jit") == hipSuccess;
+    // a failed load leaves its error as the thread's last error ("device kernel image is
+    // invalid"), which the render's launch check (hipGetLastError) would then report
+    if (!ok) (void)hipGetLastError();
+    return ok;
   };
   bool loaded = load();
   if (!loaded && k.cached) {

@@ -186,6 +186,39 @@ __device__ __forceinline__ d3 refract(d3 uv, d3 n, double e) {  // vec3.rs:223-2
   return vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), n, perp);
 }
 
+// ---------------------------------------------------------------- radiance weights
+// Quantities that only weight radiance and never steer a path -- the throughput beta, a bounce's
+// factor atten * s_pdf / pdf_val, emission, the background, PDF and scattering-PDF values, the
+// light-list PDF after its f64 hit tests -- are computed in f32 (wt / w3). Every ray, hit,
+// interval, Schlick / TIR test, random draw and every zero test that selects a branch stays f64,
+// so a path takes the same bounces (op counts identical to the f64 oracle's); only the sample's
+// radiance carries the f32 roundings (a few 2^-24 relative per bounce). v_fma_f64 issues at half
+// the f32 rate, and v_rcp_f32 / v_rsq_f32 (1 ulp) replace f64 reciprocals and roots with their
+// Newton steps. RT_F64W (A/B only): the same expressions in f64.
+#ifdef RT_F64W
+typedef double wt;
+typedef d3 w3;
+__device__ __forceinline__ w3 mkw(wt x, wt y, wt z) { return mk(x, y, z); }
+__device__ __forceinline__ w3 to_w3(d3 v) { return v; }
+__device__ __forceinline__ d3 to_d3(w3 v) { return v; }
+__device__ __forceinline__ wt rcp_wt(wt b) { return rcp_w(b); }
+__device__ __forceinline__ wt rsq_wt(wt x) { return rsq_nr(x); }
+#else
+typedef float wt;
+struct w3 {
+  float x, y, z;
+};
+__device__ __forceinline__ w3 mkw(wt x, wt y, wt z) { return {x, y, z}; }
+__device__ __forceinline__ w3 operator*(w3 a, w3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ w3 operator*(w3 a, wt t) { return {a.x * t, a.y * t, a.z * t}; }
+__device__ __forceinline__ w3 to_w3(d3 v) { return {(float)v.x, (float)v.y, (float)v.z}; }
+__device__ __forceinline__ d3 to_d3(w3 v) { return {(double)v.x, (double)v.y, (double)v.z}; }
+// 1/b within an ulp; 1/+-0 = +-inf, 1/inf = 0 and NaN stay, as the reference's weights
+__device__ __forceinline__ wt rcp_wt(wt b) { return __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ wt rsq_wt(wt x) { return __builtin_amdgcn_rsqf(x); }
+#endif
+constexpr wt kInvPiW = (wt)(1.0 / 3.14159265358979323846);
+
 // x^5 correctly rounded, for Schlick's (1 - cos)^5 (material.rs:162 calls powf(5.), i.e. the
 // platform pow). x^2 is formed exactly as a double-double (a + ae), squared and multiplied by x
 // in double-double (relative error ~2^-104), then rounded once: the IEEE-rounded x^5 except
@@ -1841,16 +1874,39 @@ __device__ __forceinline__ d3 random_unit_vector(Rng& g) {  // vec3.rs:215-217, 
   }
 }
 
+// Quad::pdf_value's weight after its f64 hit test (object.rs:492-501): dist2 / (cosine * area)
+// with dist2 = t^2 |d|^2 and cosine = |d . n| / |d| (shared by the interpreter and the generated
+// light-list PDF, rt_jit.cpp, so that both kernels compute the same bits)
+__device__ __forceinline__ wt quad_light_w(d3 dir, double t, d3 n, double area) {
+#ifdef RT_F64W
+  const double len2 = dot(dir, dir);
+  const double dist2 = (t * t) * len2;
+  const double cosine = fabs(dot(dir, n)) * rsq_nr(len2);
+  return dist2 * rcp_w(cosine * area);
+#else
+  const w3 d = to_w3(dir), nf = to_w3(n);
+  const float len2 = fmaf(d.x, d.x, fmaf(d.y, d.y, d.z * d.z));
+  const float tf = (float)t;
+  const float cosine = fabsf(fmaf(d.x, nf.x, fmaf(d.y, nf.y, d.z * nf.z))) * rsq_wt(len2);
+  return ((tf * tf) * len2) * rcp_wt(cosine * (float)area);
+#endif
+}
+// Sphere::pdf_value's weight (object.rs:190-202): 1 / (2 pi (1 - cos_theta_max)); 1 - cos in f64
+// (a small, distant sphere's cos_theta_max is within a few f32 ulps of 1)
+__device__ __forceinline__ wt sphere_light_w(double cos_max) {
+  return rcp_wt((wt)(2.0 * kPi) * (wt)(1.0 - cos_max));
+}
+
 // Light-list PDF value (HittablePDF::value pdf.rs:91-93 -> HittableList::pdf_value
 // hittable.rs:115-124 -> Quad/Sphere::pdf_value object.rs:492-501, 190-202).
 // cos_sl0: cos_theta_max of the first sphere light at `origin` (object.rs:196), computed once per
 // bounce by the caller and shared with Sphere::random (the same expression, the same bits).
 template <bool COUNT>
-__device__ double light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
-                                 double cos_sl0, Ctr<COUNT>& C) {
+__device__ wt light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
+                             double cos_sl0, Ctr<COUNT>& C) {
   const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
   uint32_t type = L[0] & 0xffu;
-  double pv = 0.0;
+  wt pv = 0;
   if (type == RTL_QUAD) {
     C.inc(RT_OP_LIGHT_PDF_QUAD);
     double t = 0.0;
@@ -1869,12 +1925,9 @@ __device__ double light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3
     } else {
       hq = quad_test<COUNT>(L, origin, dir, 0.001, kInf, t, C);
     }
-    {  // straight-line; weights: rsq/rcp Newton instead of the IEEE sqrt and divisions
-      const double len2 = dot(dir, dir);
-      const double dist2 = (t * t) * len2;
-      const double cosine = fabs(dot(dir, ld3(L, 0))) * rsq_nr(len2);
-      const double q = dist2 * rcp_w(cosine * ldd(L, 7));
-      pv = hq ? q : 0.0;
+    {
+      const wt q = quad_light_w(dir, t, ld3(L, 0), ldd(L, 7));
+      pv = hq ? q : (wt)0;
     }
   } else if (type == RTL_SPHERE) {
     C.inc(RT_OP_LIGHT_PDF_SPHERE);
@@ -1904,9 +1957,8 @@ __device__ double light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3
       double r = ldd(L, 3);
       cos_max = sqrt_nr(1.0 - r * r / dot(cmo, cmo));
     }
-    const double solid = 2.0 * kPi * (1.0 - cos_max);
-    const double q = rcp_w(solid);
-    pv = hs ? q : 0.0;
+    const wt q = sphere_light_w(cos_max);
+    pv = hs ? q : (wt)0;
   }
   return pv;  // RTL_OTHER (Object::pdf_value's default arm, object.rs:306-311): 0
 }
@@ -1914,33 +1966,33 @@ __device__ double light_leaf_pdf(const TraceParams& P, uint32_t i, d3 origin, d3
 // -> hittable.rs:115-124): the left fold of its children's values times 1/len. NEST bounds the
 // nesting below this entry (the flattener rejects deeper light lists).
 template <bool COUNT, int NEST>
-__device__ double light_entry_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
-                                  double cos_sl0, Ctr<COUNT>& C) {
+__device__ wt light_entry_pdf(const TraceParams& P, uint32_t i, d3 origin, d3 dir,
+                              double cos_sl0, Ctr<COUNT>& C) {
   const kptr L = (kptr)P.lights + ((kptr)P.light_offs)[i];
   if constexpr (NEST > 0) {
     if ((L[0] & 0xffu) == RTL_LLIST) {
       const uint32_t n = L[0] >> 8, first = L[1];
-      double sum = 0.0;
+      wt sum = 0;
       for (uint32_t k = 0; k < n; ++k) {
-        const double pv = light_entry_pdf<COUNT, NEST - 1>(P, first + k, origin, dir, cos_sl0, C);
+        const wt pv = light_entry_pdf<COUNT, NEST - 1>(P, first + k, origin, dir, cos_sl0, C);
         sum = k == 0 ? pv : sum + pv;
       }
-      return sum * ldd(L, 0);  // weight = 1 / len, the host's IEEE division
+      return sum * (wt)ldd(L, 0);  // weight = 1 / len, the host's IEEE division
     }
   }
   return light_leaf_pdf<COUNT>(P, i, origin, dir, cos_sl0, C);
 }
 template <bool COUNT>
-__device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_sl0,
-                            Ctr<COUNT>& C) {
-  double sum = 0.0;
+__device__ wt light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_sl0,
+                        Ctr<COUNT>& C) {
+  wt sum = 0;
   for (uint32_t i = 0; i < P.n_lights; ++i) {
-    const double pv = P.lights_nested
+    const wt pv = P.lights_nested
                           ? light_entry_pdf<COUNT, RTL_LIGHT_NEST>(P, i, origin, dir, cos_sl0, C)
                           : light_leaf_pdf<COUNT>(P, i, origin, dir, cos_sl0, C);
     sum = i == 0 ? pv : sum + pv;
   }
-  return P.lights_is_list ? sum * P.inv_n_lights : sum;  // weight = 1/len (hittable.rs:116)
+  return P.lights_is_list ? sum * (wt)P.inv_n_lights : sum;  // weight = 1/len (hittable.rs:116)
 }
 
 // The reference's special values (render.rs:287-292). ray_color returns
@@ -1955,7 +2007,7 @@ __device__ double light_pdf(const TraceParams& P, d3 origin, d3 dir, double cos_
 //        way, and the finite radiance gathered before it is absorbed by the inf / NaN).
 // Radiance is never negative (attenuations, emission and PDFs are >= 0), so no -inf arises.
 constexpr uint32_t RT_XS_ON = 8u;
-__device__ __forceinline__ uint32_t xs_nan_bits(d3 c, d3 beta) {
+__device__ __forceinline__ uint32_t xs_nan_bits(w3 c, w3 beta) {
   const bool nx = !(c.x != 0.0) | !(beta.x != 0.0);  // 0 or NaN
   const bool ny = !(c.y != 0.0) | !(beta.y != 0.0);
   const bool nz = !(c.z != 0.0) | !(beta.z != 0.0);
@@ -1996,8 +2048,8 @@ struct TravInterpN {
   }
   // the mixture's light-list PDF value (pdf.rs:91-93)
   template <bool COUNT>
-  static __device__ __forceinline__ double lights_pdf(const TraceParams& P, d3 origin, d3 dir,
-                                                      double cos_sl0, Ctr<COUNT>& C) {
+  static __device__ __forceinline__ wt lights_pdf(const TraceParams& P, d3 origin, d3 dir,
+                                                  double cos_sl0, Ctr<COUNT>& C) {
     return light_pdf<COUNT>(P, origin, dir, cos_sl0, C);
   }
   // the hit record's frame (transform.rs:57-135): the world ray into the winner's frame, and its
@@ -2130,11 +2182,12 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   // take the exec-masked writes of the branches as they are. (The BVH kernels' LDS holds the
   // compact trees; they keep registers, and do not spill there.)
   constexpr bool LDSF = !BVH;
-  __shared__ double sh_f[LDSF ? 3 * NB : 1];
-  __shared__ double sh_le[LDSF ? 3 * NB : 1];
+  __shared__ wt sh_f[LDSF ? 3 * NB : 1];
+  __shared__ wt sh_le[LDSF ? 3 * NB : 1];
   const int tid = threadIdx.x;
 
-  d3 ro = mk(0., 0., 0.), rd = ro, beta = ro;
+  d3 ro = mk(0., 0., 0.), rd = ro;
+  w3 beta = mkw(0, 0, 0);
   double tm = 0.;
   // remaining bounces (low 24 bits, render.rs:260) | special-value state RT_XS_* << 24
   int depth = 0;
@@ -2300,7 +2353,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       ro = origin;
       rd = ps - origin;
       tm = rnd(g);
-      beta = mk(1., 1., 1.);
+      beta = mkw(1, 1, 1);
       depth = Q->max_depth;  // RT_XS_* cleared
       alive = true;
       fresh = false;
@@ -2327,16 +2380,17 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // and a zero-pdf bounce restarts the sum at 0), so its radiance is 0 until that bounce and
     // then 0 + beta * X = beta * X exactly: no running radiance is carried across bounces.
     bool term = false, emit_end = false;
-    d3 Le;                      // the ending lanes' radiance (undefined on the others)
-    d3 p_next, d_next, f_next;  // the scattered ray and this bounce's throughput factor
-    auto set_le = [&](d3 v) {
+    w3 Le;              // the ending lanes' radiance (undefined on the others)
+    d3 p_next, d_next;  // the scattered ray
+    w3 f_next;          // this bounce's throughput factor
+    auto set_le = [&](w3 v) {
       if constexpr (LDSF) {
         sh_le[tid] = v.x, sh_le[NB + tid] = v.y, sh_le[2 * NB + tid] = v.z;
       } else {
         Le = v;
       }
     };
-    auto set_f = [&](d3 v) {
+    auto set_f = [&](w3 v) {
       if constexpr (LDSF) {
         sh_f[tid] = v.x, sh_f[NB + tid] = v.y, sh_f[2 * NB + tid] = v.z;
       } else {
@@ -2374,7 +2428,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
 #endif
     if (!Trav::template world<COUNT, VOL, BVH, VOLB, VOLI>(P, ro, rd, tm, t, hn, hf, g, C)) {
       C.inc(RT_OP_MISSES);  // background render.rs:298-309
-      set_le(beta * karr3(kparams()->bg));
+      set_le(beta * to_w3(karr3(kparams()->bg)));
       term = emit_end = true;
       break;
     }
@@ -2433,7 +2487,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     PROF(3);
     if ((SC & kScLight) && kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:210-222
       C.inc(RT_OP_EMISSIVE_HITS);
-      set_le(front ? beta * tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C) : mk(0., 0., 0.));
+      set_le(front ? beta * to_w3(tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C)) : mkw(0, 0, 0));
       term = emit_end = true;
       break;
     }
@@ -2443,7 +2497,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       d3 ruv = random_unit_vector(g);
       p_next = p;
       d_next = vfma(ldd(M, 3), ruv, unit_vector(reflected));
-      set_f(ld3(M, 0));
+      set_f(to_w3(ld3(M, 0)));
       break;
     }
     // Dielectric (material.rs:166-191), Lambertian and Isotropic (the mixture-PDF branch,
@@ -2481,10 +2535,11 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr)
     const bool refl = tir || r0s + (1.0 - r0s) * pow5_cr(1.0 - cos_t) > u0;
     const bool light_branch = !diel && have_lights && u0 < 0.5;
-    d3 dir, factor;  // set on both arms below
+    d3 dir;     // set on both arms below
+    w3 factor;
     double cos_sl = cos_sl0;
     if (!diel) {
-      d3 atten = tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C);
+      const w3 atten = to_w3(tex_value<COUNT, TEX>(P, T, mh.y, u, v, p, C));
       // Draw order as the reference: mixture coin (above), then light index
       // (hittable.rs:126-129) or nothing, then the two uniforms of whichever generator runs.
       uint32_t ltype = 0, li = 0;
@@ -2555,37 +2610,40 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
         }
         dir = local;
       }
-      double mat_pdf, s_pdf;
+      wt mat_pdf, s_pdf;
       if (iso) {
-        mat_pdf = 1.0 / (4.0 * kPi);                   // SpherePDF::value pdf.rs:47-49
-        s_pdf = iso_ref ? 0.0 : 1.0 / (4.0 * kPi);     // semantics S2 (material.rs:70-72)
+        mat_pdf = (wt)(1.0 / (4.0 * kPi));                      // SpherePDF::value pdf.rs:47-49
+        s_pdf = iso_ref ? (wt)0 : (wt)(1.0 / (4.0 * kPi));      // semantics S2 (material.rs:70-72)
       } else {
-        d3 udir = unit_vector(dir);
-        double cv = dot(udir, un) * (1.0 / kPi);       // CosinePDF::value pdf.rs:69-73
-        mat_pdf = cv > 0.0 ? cv : 0.0;
-        double csn = dot(normal, udir);                // Lambertian::scattering_pdf 100-108
-        s_pdf = csn < 0.0 ? 0.0 : csn * (1.0 / kPi);
+        // CosinePDF::value (pdf.rs:69-73) and Lambertian::scattering_pdf (material.rs:100-108):
+        // the cosines of unit(dir) with w = unit(normal) and with the normal. Their zero tests
+        // take the signs of the f64 dot products with dir (1/|dir| > 0 keeps a sign); the values
+        // are weights: the f32 dots scaled by 1/|dir|.
+        const double dw = dot(dir, un), dn = dot(normal, dir);
+        const wt irs = rsq_wt((wt)dot(dir, dir)) * kInvPiW;
+        mat_pdf = dw > 0.0 ? (wt)dw * irs : (wt)0;
+        s_pdf = dn < 0.0 ? (wt)0 : (wt)dn * irs;
       }
-      double pdf_val = mat_pdf;
+      wt pdf_val = mat_pdf;
       PROF(5);
 #ifndef RT_ABL_NOLPDF  // ablation build: no light-PDF evaluation (weights only; same paths)
       if (have_lights)  // pdf.rs:116
-        pdf_val = fma(0.5, Trav::template lights_pdf<COUNT>(P, p, dir, cos_sl, C), 0.5 * mat_pdf);
+        pdf_val = fma((wt)0.5, Trav::template lights_pdf<COUNT>(P, p, dir, cos_sl, C), (wt)0.5 * mat_pdf);
 #ifdef RT_ABL_LPDF2  // ablation build: the light PDF evaluated twice (same result)
       if (have_lights) {
         d3 p2 = p;
         asm volatile("" : "+v"(p2.x));
-        const double lp2 = Trav::template lights_pdf<COUNT>(P, p2, dir, cos_sl, C);
+        const wt lp2 = Trav::template lights_pdf<COUNT>(P, p2, dir, cos_sl, C);
         asm volatile("" ::"v"(lp2));
       }
 #endif
 #endif
       PROF(6);
-      factor = atten * (s_pdf * rcp_w(pdf_val));
+      factor = atten * (s_pdf * rcp_wt(pdf_val));
 #ifndef RT_ABL_NOXS  // ablation build: no special-value tracking (cost of RT_XS_*)
-      if (!(pdf_val != 0.0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
+      if (!(pdf_val != (wt)0)) {  // pdf_val 0 or NaN: the sample becomes inf / NaN (RT_XS_ON)
         depth |= (int)((RT_XS_ON | xs_nan_bits(atten * s_pdf, beta)) << 24);
-        beta = mk(1., 1., 1.);
+        beta = mkw(1, 1, 1);
         factor = beta;
       }
 #endif
@@ -2594,7 +2652,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
       const d3 perp = ratio * vfma(cos_t, normal, uu);
       const d3 refr = vfma(-sqrt_nr(fabs(1.0 - dot(perp, perp))), normal, perp);
       dir = refl ? reflect(uu, normal) : refr;
-      factor = ld3(M, 0);  // attenuation = tint
+      factor = to_w3(ld3(M, 0));  // attenuation = tint
     }
     p_next = p;
     d_next = dir;
@@ -2603,7 +2661,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (run) {  // wave-uniform: commit the bounce (garbage on ending lanes, never read)
       ro = p_next;
       rd = d_next;
-      if constexpr (LDSF) f_next = mk(sh_f[tid], sh_f[NB + tid], sh_f[2 * NB + tid]);
+      if constexpr (LDSF) f_next = mkw(sh_f[tid], sh_f[NB + tid], sh_f[2 * NB + tid]);
       beta = beta * f_next;
       // the product is formed here: left to itself the compiler sinks it to beta's next use (the
       // following bounce, past the pool scheduling and the camera-ray block), which keeps the
@@ -2617,9 +2675,9 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     }
     if (term & alive) {
       if constexpr (LDSF) {
-        if (emit_end) Le = mk(sh_le[tid], sh_le[NB + tid], sh_le[2 * NB + tid]);
+        if (emit_end) Le = mkw(sh_le[tid], sh_le[NB + tid], sh_le[2 * NB + tid]);
       }
-      end_sample(emit_end ? Le : mk(0., 0., 0.));
+      end_sample(emit_end ? to_d3(Le) : mk(0., 0., 0.));
     }
   }
 #ifdef RT_PROF

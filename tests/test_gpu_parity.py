@@ -454,21 +454,33 @@ def test_trace_kernel_timing_history(gpu_available):
 # fourth row of the frame, 200 rows)
 def _frame_report(cfg, acc_g, acc_o, spp):
     """max |d| of the per-sample average, pixels above TOL, and pixels whose f32 sums differ by
-    more than 4 ulps (a sample that took another path; rounding moves a sum by <= 1 ulp)."""
+    more than 4 ulps (a sample that took another path, or -- since round 6 -- radiance weights
+    rounded in f32; rounding moves a sum by <= 1 ulp). Also the tail of the distribution (VERDICT
+    r5 item 5): the ten largest per-pixel |d| (per sample), the pixels above TOL / 2, and the
+    largest |d| of a pixel's sum, i.e. the radiance difference of its flipped sample(s) -- a single
+    flipped sample fails TOL only above TOL * spp (C4: 0.49). Returns (flip pixels, max |d|)."""
     fin = np.isfinite(acc_g) & np.isfinite(acc_o)
     d = np.where(fin, np.abs(acc_g.astype(np.float64) - acc_o.astype(np.float64)), 0.0)
     ulp = np.spacing(np.maximum(np.abs(acc_g), np.abs(acc_o))).astype(np.float64)
     flips = int((d > 4 * ulp).any(axis=2).sum())
+    dp = d.max(axis=2)
+    top = np.sort(dp.ravel())[-10:][::-1] / spp
     print(f"{cfg}: max |d| {d.max() / spp:.3e}, pixels > {TOL}: "
           f"{int((d / spp > TOL).any(axis=2).sum())}, flip pixels {flips} of "
           f"{acc_g.shape[0] * acc_g.shape[1]}")
-    return flips
+    print(f"{cfg}: tail: ten largest per-pixel |d| " + " ".join(f"{x:.2e}" for x in top) +
+          f"; pixels > {TOL / 2:g}: {int((dp / spp > TOL / 2).sum())}; largest sum |d| "
+          f"(flipped-sample radiance) {d.max():.4f} against {TOL * spp:.2f} that breaks {TOL}")
+    return flips, d.max() / spp
 
 
 # Flip-pixel ceilings of the five C4 bands: 1.25 x the counts at the round-4 head (753, 778, 790,
 # 712, 746; profiles/r04y_gputest.log), so a change that makes the device drift further from the
 # oracle's paths fails here although every pixel stays within TOL (VERDICT r4, weak 2).
 C4_FLIP_CEILING = {2: 941, 6: 972, 10: 987, 14: 890, 18: 932}
+# C2 / C3 whole frames (same paths as the oracle, identical op counts): max |d| per sample from
+# the f32 radiance weights alone (VERDICT r5 item 3: <= 1e-6)
+C23_TOL = 1e-6
 
 
 @pytest.mark.timeout(900)
@@ -490,9 +502,11 @@ def test_baseline_config_frames_vs_oracle(gpu_available, cfg, name, kw, rows, op
     b, s_, n = rows
     acc_g, acc_o, st = _compare(blob, cam, row_begin=b, row_step=s_, n_rows=n, ops_rtol=ops_rtol)
     assert st.samples == n * 800 * cam.samples_per_pixel
-    flips = _frame_report(cfg, acc_g, acc_o, cam.samples_per_pixel)
+    flips, dmax = _frame_report(cfg, acc_g, acc_o, cam.samples_per_pixel)
     if ops_rtol == 0.0:
-        assert flips == 0
+        # C2 / C3: every path decision identical (op counts above); only the f32 radiance weights
+        # round differently from the oracle's f64 (rt_kernel.h wt): within C23_TOL per sample
+        assert dmax <= C23_TOL, (cfg, dmax)
     else:
         assert flips <= C4_FLIP_CEILING[b], (cfg, flips)
 

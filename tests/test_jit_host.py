@@ -84,7 +84,8 @@ def test_cornell_lights_pdf_unrolled():
     assert "aquad_test<COUNT, 1>" in lp and "0.001, kInf" in lp
     assert "(0x1.aa9p+13)" in lp  # light area 130 x 105 = 13650
     assert "cos_max = cos_sl0;" in lp
-    assert "return sum * (0x1p-1);" in lp
+    assert "return sum * (wt)(0x1p-1);" in lp  # radiance weights in f32 (rt_kernel.h wt)
+    assert "quad_light_w(dir, t, " in lp and "sphere_light_w(cos_max)" in lp
     # a scene without lights: the value is never used (have_lights false), the function is 0
     blob, cam = rt.preset_blob("random_balls", width=32, spp=4)
     state, src = rt.jit_check(blob)
