@@ -202,51 +202,29 @@ static void sincos2pi(double u, double* s, double* c) {
 #endif
 
 /* =============================================================== RNG
- * Per pixel-sample stream: pcg4d(pixel, sample, seed_lo, seed_hi) seeds xoroshiro64** (Blackman
- * and Vigna; 64 bits of state, 32-bit outputs), the device's generator (csrc/rt_rng.h). Until
- * round 5 both used xoshiro128** (-DORACLE_RNG_X128 / -DRT_RNG_X128 restore it). */
-typedef struct { uint32_t s[4]; } rng_t;
+ * Per pixel-sample stream: pcg2d(pixel, sample) with seed-keyed increments seeds xoroshiro64**
+ * (Blackman and Vigna; 64 bits of state, 32-bit outputs), the device's generator
+ * (csrc/rt_rng.h rng_seed / rng_step). Round 5 keyed it with pcg4d(pixel, sample, seed_lo,
+ * seed_hi); rounds 1-4 used xoshiro128**. */
+typedef struct { uint32_t s[2]; } rng_t;
 
-static void pcg4d(uint32_t v[4]) {
-  for (int i = 0; i < 4; ++i) v[i] = v[i] * 1664525u + 1013904223u;
-  v[0] += v[1] * v[3];
-  v[1] += v[2] * v[0];
-  v[2] += v[0] * v[1];
-  v[3] += v[1] * v[2];
-  for (int i = 0; i < 4; ++i) v[i] ^= v[i] >> 16;
-  v[0] += v[1] * v[3];
-  v[1] += v[2] * v[0];
-  v[2] += v[0] * v[1];
-  v[3] += v[1] * v[2];
-}
 static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 static void rng_seed(rng_t* g, uint64_t seed, uint32_t pixel, uint32_t sample) {
-  uint32_t v[4] = {pixel, sample, (uint32_t)seed, (uint32_t)(seed >> 32)};
-  pcg4d(v);
-#ifdef ORACLE_RNG_X128
-  if ((v[0] | v[1] | v[2] | v[3]) == 0) v[0] = 0x9E3779B9u;
-#else
-  v[0] ^= v[2];  /* xoroshiro64**: the four hash words folded into 64 bits of state */
-  v[1] ^= v[3];
-  v[2] = v[3] = 0;
-  if ((v[0] | v[1]) == 0) v[0] = 0x9E3779B9u;
-#endif
-  memcpy(g->s, v, 16);
+  const uint32_t k0 = ((uint32_t)seed ^ 0x85EBCA6Bu) * 0x9E3779B9u + 1013904223u;
+  const uint32_t k1 = ((uint32_t)(seed >> 32) ^ 0xC2B2AE35u) * 0x9E3779B9u + (k0 ^ 0x27D4EB2Fu);
+  uint32_t v0 = pixel * 1664525u + k0, v1 = sample * 1664525u + k1;
+  v0 += v1 * 1664525u;
+  v1 += v0 * 1664525u;
+  v0 ^= v0 >> 16;
+  v1 ^= v1 >> 16;
+  v0 += v1 * 1664525u;
+  v1 += v0 * 1664525u;
+  v0 ^= v0 >> 16;
+  v1 ^= v1 >> 16;
+  if ((v0 | v1) == 0) v0 = 0x9E3779B9u;
+  g->s[0] = v0;
+  g->s[1] = v1;
 }
-#ifdef ORACLE_RNG_X128
-static inline uint32_t rng_u32(rng_t* g) {
-  uint32_t* s = g->s;
-  uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
-  uint32_t t = s[1] << 9;
-  s[2] ^= s[0];
-  s[3] ^= s[1];
-  s[1] ^= s[2];
-  s[0] ^= s[3];
-  s[2] ^= t;
-  s[3] = rotl32(s[3], 11);
-  return result;
-}
-#else
 static inline uint32_t rng_u32(rng_t* g) { /* xoroshiro64** */
   uint32_t* s = g->s;
   const uint32_t s0 = s[0];
@@ -257,7 +235,6 @@ static inline uint32_t rng_u32(rng_t* g) { /* xoroshiro64** */
   s[1] = rotl32(s1, 13);
   return result;
 }
-#endif
 /* random_double (utils.rs:5-7): f64 build (= the device path): 32-bit uniform in [0,1), exact
  * in double; f32 precision-study build: 24-bit uniform (representable in float). */
 #if ORACLE_F64

@@ -717,14 +717,14 @@ int flatten(const rt_scene_blob* blob, FlatScene* out, std::string* err) {
   F.perlin.assign(n_perl * RTL_PERLIN_BYTES, 0);
   for (uint64_t p = 0; p < n_perl; ++p) {
     uint64_t b = perl_off + p * RT_PERLIN_SLOTS;
-    double* rv = (double*)&F.perlin[p * RTL_PERLIN_BYTES];
+    float* rv = (float*)&F.perlin[p * RTL_PERLIN_BYTES];
     for (int k = 0; k < 256; ++k) {
-      rv[4 * k] = rd_f(b + 3 * k);
-      rv[4 * k + 1] = rd_f(b + 3 * k + 1);
-      rv[4 * k + 2] = rd_f(b + 3 * k + 2);
-      rv[4 * k + 3] = 0.0;
+      rv[4 * k] = (float)rd_f(b + 3 * k);
+      rv[4 * k + 1] = (float)rd_f(b + 3 * k + 1);
+      rv[4 * k + 2] = (float)rd_f(b + 3 * k + 2);
+      rv[4 * k + 3] = 0.0f;
     }
-    uint8_t* perm = &F.perlin[p * RTL_PERLIN_BYTES + 8192];
+    uint8_t* perm = &F.perlin[p * RTL_PERLIN_BYTES + 4096];
     for (int k = 0; k < 768; ++k) {
       int64_t v = (int64_t)s[b + 768 + k];
       if (v < 0 || v > 255) {

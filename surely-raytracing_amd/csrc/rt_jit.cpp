@@ -720,9 +720,6 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_RNG2
   opts.push_back("-DRT_ABL_RNG2");
 #endif
-#ifdef RT_RNG_X128
-  opts.push_back("-DRT_RNG_X128");
-#endif
   // diagnostics: extra compiler options, space separated (register-allocation A/B)
   std::vector<std::string> extra;
   if (const char* e = std::getenv("RT_JIT_OPTS")) {

@@ -1730,51 +1730,52 @@ __device__ __forceinline__ uint32_t f2u_sat(double f) {  // Rust `as u32`
 }
 
 // Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96. T = one table
-// (RTL_PERLIN_BYTES: ranvec as 256 double4, then perm_x/y/z), normally the workgroup's LDS copy
-// (rt_trace stages the scene's first kPerlinLds tables at launch). The octave loop stays rolled
-// and each octave reads the six permutation entries once, so the eight corner gathers are the
-// only wide live values.
-__device__ __forceinline__ double perlin_turb(const uint8_t* __restrict__ T, d3 p) {
-  const double* rv = reinterpret_cast<const double*>(T);
-  const uint8_t* px = T + 8192;
+// (RTL_PERLIN_BYTES: ranvec as 256 float4, then perm_x/y/z), normally the workgroup's LDS copy
+// (rt_trace stages the scene's first kPerlinLds tables at launch). The turbulence only colours a
+// noise texture (a weight, rt_kernel.h wt), so it is computed in f32 -- except the lattice cell
+// and the offset in it: floor(p) and p - floor(p) are exact in f64 (p doubles per octave, also
+// exact), so every lane reads the reference's eight corners; the offsets are then rounded to f32.
+// The octave loop stays rolled and each octave reads the six permutation entries once, so the
+// eight corner gathers (one 16-byte read each) are the only wide live values.
+__device__ __forceinline__ float perlin_turb(const uint8_t* __restrict__ T, d3 p) {
+  const float4* rv = reinterpret_cast<const float4*>(T);
+  const uint8_t* px = T + 4096;
   const uint8_t* py = px + 256;
   const uint8_t* pz = py + 256;
-  double accum = 0.0, weight = 1.0;
+  float accum = 0.0f, weight = 1.0f;
 #pragma unroll 1
   for (int oct = 0; oct < 7; ++oct) {
-    double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
-    double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    const float u = (float)(p.x - fx), v = (float)(p.y - fy), w = (float)(p.z - fz);
     const uint32_t i = (uint32_t)f2i_sat(fx), j = (uint32_t)f2i_sat(fy), k = (uint32_t)f2i_sat(fz);
     const uint32_t X[2] = {px[i & 255u], px[(i + 1u) & 255u]};
     const uint32_t Y[2] = {py[j & 255u], py[(j + 1u) & 255u]};
     const uint32_t Z[2] = {pz[k & 255u], pz[(k + 1u) & 255u]};
-    double uu = u * u * (3.0 - 2.0 * u);
-    double vv = v * v * (3.0 - 2.0 * v);
-    double ww = w * w * (3.0 - 2.0 * w);
-    double acc = 0.0;
+    const float uu = u * u * (3.0f - 2.0f * u);
+    const float vv = v * v * (3.0f - 2.0f * v);
+    const float ww = w * w * (3.0f - 2.0f * w);
+    float acc = 0.0f;
 #pragma unroll
     for (int di = 0; di < 2; ++di)
 #pragma unroll
       for (int dj = 0; dj < 2; ++dj)
 #pragma unroll
         for (int dk = 0; dk < 2; ++dk) {
-          const uint32_t idx = X[di] ^ Y[dj] ^ Z[dk];
-          double2 cxy = *reinterpret_cast<const double2*>(rv + 4 * idx);
-          d3 c = mk(cxy.x, cxy.y, rv[4 * idx + 2]);
-          double wi = di ? uu : 1.0 - uu;
-          double wj = dj ? vv : 1.0 - vv;
-          double wk = dk ? ww : 1.0 - ww;
-          d3 wv = mk(u - (double)di, v - (double)dj, w - (double)dk);
-          acc = fma(wi * wj * wk, dot(c, wv), acc);
+          const float4 c = rv[X[di] ^ Y[dj] ^ Z[dk]];
+          const float wi = di ? uu : 1.0f - uu;
+          const float wj = dj ? vv : 1.0f - vv;
+          const float wk = dk ? ww : 1.0f - ww;
+          const float d = fmaf(c.x, u - (float)di, fmaf(c.y, v - (float)dj, c.z * (w - (float)dk)));
+          acc = fmaf(wi * wj * wk, d, acc);
         }
-    accum = fma(weight, acc, accum);
-    weight *= 0.5;
+    accum = fmaf(weight, acc, accum);
+    weight *= 0.5f;
     p = p * 2.0;
   }
-  return fabs(accum);
+  return fabsf(accum);
 }
 // Tables past the LDS-staged ones (scenes with more than kPerlinLds noise textures): global.
-__device__ __noinline__ double perlin_turb_global(const uint8_t* __restrict__ T, d3 p) {
+__device__ __noinline__ float perlin_turb_global(const uint8_t* __restrict__ T, d3 p) {
   return perlin_turb(T, p);
 }
 
@@ -1812,18 +1813,18 @@ __device__ d3 tex_value(const TraceParams& P, const TT& T, uint32_t id, double u
     if (h.x == RT_TEX_NOISE) {  // texture.rs:127-130
       C.inc(RT_OP_NOISE_EVALS);
       d3 s = p * ldd(t, 0);
-      double turb = h.y < P.n_perlin_lds
+      const float turb = h.y < P.n_perlin_lds
                         ? perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s)
                         : perlin_turb_global(P.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s);
 #ifdef RT_ABL_NOISE2  // ablation build: the turbulence evaluated twice (same result; its cost)
       {
         d3 s2 = s;
         asm volatile("" : "+v"(s2.x));
-        const double t2 = perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s2);
+        const float t2 = perlin_turb(T.perlin + (size_t)h.y * RTL_PERLIN_BYTES, s2);
         asm volatile("" ::"v"(t2));
       }
 #endif
-      double k = 0.5 * (1.0 + sin(fma(10.0, turb, s.z)));
+      double k = 0.5 * (1.0 + sin(fma(10.0, (double)turb, s.z)));
       return mk(k, k, k);
     }
     break;
@@ -2197,9 +2198,9 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   uint32_t sij = 0;    // row item << 31 | s_j << 16 | s_i of the sample in flight
   uint32_t oslot = 0;  // the item's output value (TraceParams::part: slot * 64 + pixel in tile)
   int next = 0;        // pool items claimed so far (wave-uniform)
-  // a valid (non-zero) xoshiro state from the start: lanes without a path still run bounces on
+  // a valid (non-zero) xoroshiro64** state from the start: lanes without a path still run bounces on
   // stale rays at the end of a launch, and the rejection loops (random_unit_vector) must end
-  Rng g = {0x9E3779B9u, 1u, 2u, 3u};
+  Rng g = {0x9E3779B9u, 1u};
   // A sample's radiance is final: add it to the item's running sum. Inside a block the item
   // continues with its next s_i; at a block end a segment (or tail) item writes its f64 sum, a
   // row item adds it to its row total and goes on, writing the total after its last block.

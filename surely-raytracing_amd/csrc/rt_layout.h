@@ -155,8 +155,9 @@
  *   SOLID: d0-2 color; CHECKER: d0 inv_scale, a even, b odd;
  *   IMAGE: a width, b height, c byte offset into texels; NOISE: d0 scale, a perlin index */
 #define RTL_TEX_WORDS 12
-/* perlin table: ranvec 256 x double4 (8192 B) + perm_x/y/z 3 x 256 bytes (768 B) */
-#define RTL_PERLIN_BYTES (8192 + 768)
+/* perlin table: ranvec 256 x float4 (x, y, z, 0; 4096 B: the turbulence is a radiance weight,
+ * rt_kernel.h perlin_turb) + perm_x/y/z 3 x 256 bytes (768 B) */
+#define RTL_PERLIN_BYTES (4096 + 768)
 
 /* light entries: node-format QUAD / SPHERE / OTHER records in their own word array */
 typedef struct rtl_scene_header {

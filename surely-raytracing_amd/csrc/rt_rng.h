@@ -3,13 +3,14 @@
 // The reference draws every random number from rand::thread_rng (ChaCha12, OS-seeded,
 // utils.rs:5-15), so it is unseeded and its draw order depends on rayon scheduling. Here each
 // pixel-sample owns an independent stream keyed by (seed, global pixel index, sample index):
-// pcg4d (Jarzynski & Olano 2020) hashes the key into the state of xoroshiro64** (64 bits of
+// pcg2d (Jarzynski & Olano 2020) hashes the key into the state of xoroshiro64** (64 bits of
 // state: two VGPRs); draws are then consumed in exactly the reference's call order. Results are
 // reproducible and independent of how pixels are distributed over lanes, waves or GPUs. The CPU
 // oracle implements the same generator (oracle/rt_oracle.c). Round 5 replaced xoshiro128**
-// (RT_RNG_X128 restores it): the generator step was 8.2 % of C2 and 17.5 % of C3 by the
-// RT_ABL_RNG2 ablation (profiles/r05h_abl_rng_c{2,3}.log), and xoroshiro64**'s shorter step and
-// state took 0.4 % / 0.95 % off their kernel time (profiles/r05h_x64_c{2,3}.log).
+// (removed in round 6): the generator step was 8.2 % of C2 and 17.5 % of C3 by the RT_ABL_RNG2
+// ablation (profiles/r05h_abl_rng_c{2,3}.log), and xoroshiro64**'s shorter step and state took
+// 0.4 % / 0.95 % off their kernel time (profiles/r05h_x64_c{2,3}.log). Round 6 keyed it with
+// pcg2d instead of pcg4d (rng_seed).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,11 +18,17 @@
 namespace rtd {
 
 struct Rng {
-  uint32_t s0, s1, s2, s3;
+  uint32_t s0, s1;
 };
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+// The stream key: pcg2d (Jarzynski & Olano 2020) of (pixel, sample), its two LCG increments keyed
+// by the 64-bit seed. Every step is a bijection, so distinct (pixel, sample) pairs of one seed get
+// distinct states. The seed words are wave-uniform (scalar ALU); per lane the hash costs six
+// v_mul_lo_u32 where round 5's pcg4d of (pixel, sample, seed_lo, seed_hi) cost ten, and the
+// camera-ray block that seeds runs in nearly every bounce iteration of a wave.
 __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel,
                                         uint32_t sample) {
+#ifdef RT_SEED_PCG4D  // A/B only: round 5's key (a different stream; the oracle follows the default)
   uint32_t v0 = pixel * 1664525u + 1013904223u, v1 = sample * 1664525u + 1013904223u;
   uint32_t v2 = seed_lo * 1664525u + 1013904223u, v3 = seed_hi * 1664525u + 1013904223u;
   v0 += v1 * v3;
@@ -36,18 +43,24 @@ __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint
   v1 += v2 * v0;
   v2 += v0 * v1;
   v3 += v1 * v2;
-#ifndef RT_RNG_X128
-  // xoroshiro64**: a 64-bit state from the four hash words
   v0 ^= v2;
   v1 ^= v3;
-  if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;
-  return {v0, v1, 0u, 0u};
 #else
-  if ((v0 | v1 | v2 | v3) == 0u) v0 = 0x9E3779B9u;
-  return {v0, v1, v2, v3};
+  const uint32_t k0 = (seed_lo ^ 0x85EBCA6Bu) * 0x9E3779B9u + 1013904223u;
+  const uint32_t k1 = (seed_hi ^ 0xC2B2AE35u) * 0x9E3779B9u + (k0 ^ 0x27D4EB2Fu);
+  uint32_t v0 = pixel * 1664525u + k0, v1 = sample * 1664525u + k1;
+  v0 += v1 * 1664525u;
+  v1 += v0 * 1664525u;
+  v0 ^= v0 >> 16;
+  v1 ^= v1 >> 16;
+  v0 += v1 * 1664525u;
+  v1 += v0 * 1664525u;
+  v0 ^= v0 >> 16;
+  v1 ^= v1 >> 16;
 #endif
+  if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;  // xoroshiro64**'s state must not be all zero
+  return {v0, v1};
 }
-#ifndef RT_RNG_X128
 // xoroshiro64** (Blackman and Vigna): 32-bit outputs from 64 bits of state
 __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   const uint32_t s0 = g.s0;
@@ -58,27 +71,14 @@ __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   g.s1 = rotl32(s1, 13);
   return result;
 }
-#else
-__device__ __forceinline__ uint32_t rng_step(Rng& g) {
-  uint32_t result = rotl32(g.s1 * 5u, 7) * 9u;
-  uint32_t t = g.s1 << 9;
-  g.s2 ^= g.s0;
-  g.s3 ^= g.s1;
-  g.s1 ^= g.s2;
-  g.s0 ^= g.s3;
-  g.s2 ^= t;
-  g.s3 = rotl32(g.s3, 11);
-  return result;
-}
-#endif
 #ifdef RT_ABL_RNG2
 // ablation build (not shipped): every draw's generator step also runs on a copy of the state,
 // whose result is discarded (same image); the time delta is the generator's cost
 __device__ __forceinline__ uint32_t rng_u32(Rng& g) {
   Rng c = g;
-  asm volatile("" : "+v"(c.s0), "+v"(c.s1), "+v"(c.s2), "+v"(c.s3));
+  asm volatile("" : "+v"(c.s0), "+v"(c.s1));
   const uint32_t x = rng_step(c);
-  asm volatile("" ::"v"(x), "v"(c.s0), "v"(c.s1), "v"(c.s2), "v"(c.s3));
+  asm volatile("" ::"v"(x), "v"(c.s0), "v"(c.s1));
   return rng_step(g);
 }
 #else

@@ -85,5 +85,5 @@ def test_compact_bvhs_fit_the_lds_budget():
     n_leaves = 400 + 1000
     n_int = n_leaves - 2
     assert n_int * 52 + n_leaves * 4 <= st2["compact_bvh_bytes"] <= n_int * 52 + n_leaves * 4 + 32
-    stacks, sums, perlin = 16 * 768 * 4, 768 * 24, 8960
+    stacks, sums, perlin = 16 * 768 * 4, 768 * 24, 4864
     assert st2["compact_bvh_bytes"] + stacks + sums + perlin + 512 <= 160 * 1024
