@@ -669,6 +669,9 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_MIN_WAVES_GEN
   opts.push_back("-DRT_MIN_WAVES_GEN=" RTJ_STR(RT_MIN_WAVES_GEN));
 #endif
+#ifdef RT_MIN_WAVES_GEN_VOL
+  opts.push_back("-DRT_MIN_WAVES_GEN_VOL=" RTJ_STR(RT_MIN_WAVES_GEN_VOL));
+#endif
 #ifdef RT_BLOCK_BVH
   opts.push_back("-DRT_BLOCK_BVH=" RTJ_STR(RT_BLOCK_BVH));
 #endif

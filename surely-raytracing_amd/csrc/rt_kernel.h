@@ -71,14 +71,20 @@ constexpr size_t kLdsTotal = 160u << 10;
 #define RT_MIN_WAVES_BVH 3
 #endif
 // Scene-specialised kernels without a BVH (rt_jit.cpp) carry less code (the scene set, §4.1b
-// of DESIGN.md: cornell_box 90, cornell_smoke 100 VGPRs) and run five waves per SIMD:
-// cornell_smoke 96.65 -> 95.78 ms, cornell_box unchanged (profiles/r03_ab_occ_*.log).
+// of DESIGN.md) and run more waves per SIMD: five from round 3 (cornell_smoke 96.65 -> 95.78 ms,
+// profiles/r03_ab_occ_*.log). Round 6: the f32 radiance weights took cornell_box to 84 VGPRs;
+// at six waves (80, a few cold values spilled) it runs -0.67 %, cornell_smoke (ConstantMedium
+// kernels, RT_MIN_WAVES_GEN_VOL) -0.03 %, so those stay at five (profiles/r06e_ab_waves_c{2,3}.log).
 #ifndef RT_MIN_WAVES_GEN
-#define RT_MIN_WAVES_GEN 5
+#define RT_MIN_WAVES_GEN 6
+#endif
+#ifndef RT_MIN_WAVES_GEN_VOL
+#define RT_MIN_WAVES_GEN_VOL 5
 #endif
 template <bool VOL, bool TEX, bool BVH, bool GEN = false>
 struct MinWaves {
-  static constexpr int value = BVH ? RT_MIN_WAVES_BVH : (GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES);
+  static constexpr int value =
+      BVH ? RT_MIN_WAVES_BVH : (GEN ? (VOL ? RT_MIN_WAVES_GEN_VOL : RT_MIN_WAVES_GEN) : RT_MIN_WAVES);
 };
 
 struct d3 {

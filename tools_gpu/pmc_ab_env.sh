@@ -15,7 +15,8 @@ for SPEC in "$@"; do
   [ "$SPEC" != "-" ] && ENVS=$(echo "$SPEC" | tr ',' ' ')
   j=0
   for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR" \
-             "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA"; do
+             "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA" \
+             ${PMC_EXTRA:+"$PMC_EXTRA"}; do
     j=$((j+1))
     env $ENVS timeout -k 10 120 rocprofv3 --pmc $SET --kernel-trace -d $D/p$j -o run --output-format csv -- python3 tools_gpu/one_render.py $SC 800 $SPP > $D/p$j.log 2>&1 || exit $?
   done
