@@ -202,10 +202,10 @@ static void sincos2pi(double u, double* s, double* c) {
 #endif
 
 /* =============================================================== RNG
- * Per pixel-sample stream: pcg2d(pixel, sample) with seed-keyed increments seeds xoroshiro64**
+ * Per pixel-sample stream: pcg2d(pixel, sample) with seed-keyed increments seeds xoroshiro64*
  * (Blackman and Vigna; 64 bits of state, 32-bit outputs), the device's generator
- * (csrc/rt_rng.h rng_seed / rng_step). Round 5 keyed it with pcg4d(pixel, sample, seed_lo,
- * seed_hi); rounds 1-4 used xoshiro128**. */
+ * (csrc/rt_rng.h rng_seed / rng_step). Round 5 keyed xoroshiro64** with pcg4d(pixel, sample,
+ * seed_lo, seed_hi); rounds 1-4 used xoshiro128**. */
 typedef struct { uint32_t s[2]; } rng_t;
 
 static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
@@ -225,11 +225,11 @@ static void rng_seed(rng_t* g, uint64_t seed, uint32_t pixel, uint32_t sample) {
   g->s[0] = v0;
   g->s[1] = v1;
 }
-static inline uint32_t rng_u32(rng_t* g) { /* xoroshiro64** */
+static inline uint32_t rng_u32(rng_t* g) { /* xoroshiro64* */
   uint32_t* s = g->s;
   const uint32_t s0 = s[0];
   uint32_t s1 = s[1];
-  const uint32_t result = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
+  const uint32_t result = s0 * 0x9E3779BBu;
   s1 ^= s0;
   s[0] = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
   s[1] = rotl32(s1, 13);

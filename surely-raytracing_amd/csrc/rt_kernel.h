@@ -2204,7 +2204,7 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
   uint32_t sij = 0;    // row item << 31 | s_j << 16 | s_i of the sample in flight
   uint32_t oslot = 0;  // the item's output value (TraceParams::part: slot * 64 + pixel in tile)
   int next = 0;        // pool items claimed so far (wave-uniform)
-  // a valid (non-zero) xoroshiro64** state from the start: lanes without a path still run bounces on
+  // a valid (non-zero) xoroshiro64* state from the start: lanes without a path still run bounces on
   // stale rays at the end of a launch, and the rejection loops (random_unit_vector) must end
   Rng g = {0x9E3779B9u, 1u};
   // A sample's radiance is final: add it to the item's running sum. Inside a block the item

@@ -3,14 +3,14 @@
 // The reference draws every random number from rand::thread_rng (ChaCha12, OS-seeded,
 // utils.rs:5-15), so it is unseeded and its draw order depends on rayon scheduling. Here each
 // pixel-sample owns an independent stream keyed by (seed, global pixel index, sample index):
-// pcg2d (Jarzynski & Olano 2020) hashes the key into the state of xoroshiro64** (64 bits of
+// pcg2d (Jarzynski & Olano 2020) hashes the key into the state of xoroshiro64* (64 bits of
 // state: two VGPRs); draws are then consumed in exactly the reference's call order. Results are
 // reproducible and independent of how pixels are distributed over lanes, waves or GPUs. The CPU
 // oracle implements the same generator (oracle/rt_oracle.c). Round 5 replaced xoshiro128**
 // (removed in round 6): the generator step was 8.2 % of C2 and 17.5 % of C3 by the RT_ABL_RNG2
 // ablation (profiles/r05h_abl_rng_c{2,3}.log), and xoroshiro64**'s shorter step and state took
 // 0.4 % / 0.95 % off their kernel time (profiles/r05h_x64_c{2,3}.log). Round 6 keyed it with
-// pcg2d instead of pcg4d (rng_seed).
+// pcg2d instead of pcg4d (rng_seed) and took the * scrambler (rng_step).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -58,14 +58,22 @@ __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint
   v0 ^= v0 >> 16;
   v1 ^= v1 >> 16;
 #endif
-  if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;  // xoroshiro64**'s state must not be all zero
+  if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;  // xoroshiro64*'s state must not be all zero
   return {v0, v1};
 }
-// xoroshiro64** (Blackman and Vigna): 32-bit outputs from 64 bits of state
+// xoroshiro64* (Blackman and Vigna): 32-bit outputs from 64 bits of state. The * scrambler (one
+// multiply) is the authors' generator for floating-point draws: its weak lowest bits land below
+// 2^-24 of a draw (random_double) or are discarded (random_int, a multiply-high). Round 5 used the
+// ** scrambler (a rotate and a second multiply on top); RT_RNG_STARSTAR restores it for A/B only
+// (a different stream: the oracle follows the default).
 __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   const uint32_t s0 = g.s0;
   uint32_t s1 = g.s1;
+#ifdef RT_RNG_STARSTAR
   const uint32_t result = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
+#else
+  const uint32_t result = s0 * 0x9E3779BBu;
+#endif
   s1 ^= s0;
   g.s0 = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
   g.s1 = rotl32(s1, 13);
