@@ -1723,16 +1723,28 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
 }
 
 // ---------------------------------------------------------------- textures
-__device__ __forceinline__ int32_t f2i_sat(double f) {  // Rust `as i32`
+// Rust `as i32` / `as u32` (truncation, saturation at the type's range, NaN -> 0) is exactly what
+// v_cvt_i32_f64 / v_cvt_u32_f64 compute; C++ leaves out-of-range conversions undefined, so the
+// instructions are issued directly (the compiler made each range check a branch; C4 -1.4 %,
+// profiles/r06i_ab_noise_c4.log; tests/test_gpu_parity.py::test_saturating_texture_coordinates)
+#ifdef RT_F2I_BRANCH  // A/B only: the range checks in C++
+__device__ __forceinline__ int32_t f2i_sat(double f) {
   if (f != f) return 0;
   if (f >= 2147483648.0) return 2147483647;
   if (f <= -2147483648.0) return -2147483647 - 1;
   return (int32_t)f;
 }
-__device__ __forceinline__ uint32_t f2u_sat(double f) {  // Rust `as u32`
-  if (f != f || f <= 0.0) return 0u;
-  if (f >= 4294967296.0) return 4294967295u;
-  return (uint32_t)f;
+#else
+__device__ __forceinline__ int32_t f2i_sat(double f) {
+  int32_t r;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+}
+#endif
+__device__ __forceinline__ uint32_t f2u_sat(double f) {
+  uint32_t r;
+  asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(f));
+  return r;
 }
 
 // Perlin::turb perlin.rs:56-72 over noise 30-54 + trilinear_interp 74-96. T = one table
@@ -1760,7 +1772,11 @@ __device__ __forceinline__ float perlin_turb(const uint8_t* __restrict__ T, d3 p
     const float uu = u * u * (3.0f - 2.0f * u);
     const float vv = v * v * (3.0f - 2.0f * v);
     const float ww = w * w * (3.0f - 2.0f * w);
-    float acc = 0.0f;
+    // trilinear_interp (perlin.rs:74-96): the sum over the eight corners of
+    // (i uu + (1-i)(1-uu)) (j vv + (1-j)(1-vv)) (k ww + (1-k)(1-ww)) (c . (u-i, v-j, w-k)),
+    // formed as nested lerps (the same polynomial; 7 lerps instead of 8 weight products, within
+    // noise of them at C4: profiles/r06i_ab_noise_c4.log)
+    float dd[2][2][2];
 #pragma unroll
     for (int di = 0; di < 2; ++di)
 #pragma unroll
@@ -1768,12 +1784,12 @@ __device__ __forceinline__ float perlin_turb(const uint8_t* __restrict__ T, d3 p
 #pragma unroll
         for (int dk = 0; dk < 2; ++dk) {
           const float4 c = rv[X[di] ^ Y[dj] ^ Z[dk]];
-          const float wi = di ? uu : 1.0f - uu;
-          const float wj = dj ? vv : 1.0f - vv;
-          const float wk = dk ? ww : 1.0f - ww;
-          const float d = fmaf(c.x, u - (float)di, fmaf(c.y, v - (float)dj, c.z * (w - (float)dk)));
-          acc = fmaf(wi * wj * wk, d, acc);
+          dd[di][dj][dk] = fmaf(c.x, u - (float)di, fmaf(c.y, v - (float)dj, c.z * (w - (float)dk)));
         }
+    auto lerp = [](float a, float b, float t) { return fmaf(t, b - a, a); };
+    const float x0 = lerp(lerp(dd[0][0][0], dd[0][0][1], ww), lerp(dd[0][1][0], dd[0][1][1], ww), vv);
+    const float x1 = lerp(lerp(dd[1][0][0], dd[1][0][1], ww), lerp(dd[1][1][0], dd[1][1][1], ww), vv);
+    const float acc = lerp(x0, x1, uu);
     accum = fmaf(weight, acc, accum);
     weight *= 0.5f;
     p = p * 2.0;

@@ -139,6 +139,30 @@ def test_image_texture_parity(gpu_available):
     _compare(blob, cam)
 
 
+def test_saturating_texture_coordinates(gpu_available):
+    """Rust's saturating `as i32` (texture.rs:71-81 CheckerTexture; the same conversion takes the
+    Perlin lattice cell, perlin.rs:30-54) on coordinates far outside the i32 range: a checker of
+    scale 1e-10 (floor(1e10 p) saturates to i32::MAX / MIN, whose parity picks the colour) on
+    quads whose every coordinate has |p| >= 1, beside a noise-textured sphere. The device issues
+    v_cvt_i32_f64 directly (rt_kernel.h f2i_sat); the oracle restates the Rust cast. (A noise
+    scale that saturates the lattice, ~1e9 at these coordinates, makes the turbulence depend on
+    the hit point's last bits times 1e9 -- 3e-3 between the device and the oracle,
+    tools_gpu/diag_sat.py -- so the noise keeps an ordinary scale.)"""
+    sc = rt.Scene(12)
+    chk = sc.lambertian(tex=sc.checker_from_color(1e-10, (0.9, 0.1, 0.1), (0.1, 0.9, 0.1)))
+    marble = sc.lambertian(tex=sc.noise_texture(4.0))
+    light = sc.diffuse_light((6, 6, 6))
+    world = sc.hittable_list(sc.quad((1, -1, 1), (4, 0, 0), (0, 0, 4), chk),
+                             sc.quad((-1, -1, 1), (0, 3, 0), (0, 0, 4), chk),
+                             sc.sphere((3, 1, 3), 0.8, marble),
+                             sc.quad((1, 4, 1), (2, 0, 0), (0, 0, 2), light))
+    lights = sc.hittable_list(sc.quad((1, 4, 1), (2, 0, 0), (0, 0, 2), light))
+    blob = sc.serialize(world, lights)
+    cam = rt.camera_new(1.0, 64, 16, 20, 50, (6, 3, -3), (2, 0, 3), (0, 1, 0), 0, 0, (0.1, 0.1, 0.1))
+    acc_g, _, st = _compare(blob, cam)
+    assert st.op_counts()["noise_evals"] > 0
+
+
 def test_checker_volume_transform_mix(gpu_available):
     """Nested Translate(RotateY(BVH)) + ConstantMedium over a rotated box + checker + metal."""
     sc = rt.Scene(11)
