@@ -58,3 +58,5 @@ for i, o in enumerate(SETS):
     print(f"{o or 'default':40s} best min {mn:9.3f} ms ({100 * (mn / base - 1):+.2f} %)  "
           f"max|d|/spp {d[fin].max() if fin.any() else float('nan'):.3e}  "
           f"nan/inf mask equal {bool(np.array_equal(np.isfinite(img), np.isfinite(ref)))}", flush=True)
+for i in range(len(SETS)):  # the images are large; gpurun copies back at most 64 MiB
+    os.remove(f"{OUT}/set{i}.npy")
