@@ -693,9 +693,6 @@ int compile(const std::string& src, const std::string& arch, std::vector<char>* 
 #ifdef RT_ABL_TWICE_BVH
   opts.push_back("-DRT_ABL_TWICE_BVH=" RTJ_STR(RT_ABL_TWICE_BVH));
 #endif
-#ifdef RT_NO_PK_BOX
-  opts.push_back("-DRT_NO_PK_BOX");
-#endif
 #ifdef RT_ABL_NOXS
   opts.push_back("-DRT_ABL_NOXS");
 #endif

@@ -1201,11 +1201,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <class F>
 __device__ __forceinline__ void obvh_leaf(const gptr N, uint32_t rec, d3 o, d3 d, d3 r, double tm,
                                           double tmin, F& cand) {
-#ifdef RT_NO_BOX_LEAF  // A/B: every side of a box leaf tested (the batch loop below)
-  const bool box = false;
-#else
   const bool box = (rec & RTL_LEAF_BOX) != 0u;
-#endif
   rec &= ~RTL_LEAF_BOX;
   if (box && tmin >= 0.0) {
     // make_box's six sides (object.rs:509-560; rt_obvh.cpp make_box_batch): 0 z = max, 1 x = max,
@@ -1337,10 +1333,8 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
   constexpr float kBoxRel = 0x1p-20f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
-#ifndef RT_NO_PK_BOX
   const f32x2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
   const f32x2 ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
-#endif
   const float tmin_f = (float)(tmin - fabs(tmin) * 0x1p-20);
   double closest = tmax;
   float close_f = (float)(closest + closest * (2.0 * kTieRel));
@@ -1370,7 +1364,6 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
     while (e < hd.x) {
       s = S[2 * e];
       const uint4 s2 = S[2 * e + 1];
-#ifndef RT_NO_PK_BOX
       // (near, far) bound pairs: one packed f32 subtract and multiply per axis (v_pk_add_f32,
       // v_pk_mul_f32), the same two roundings per slab time as the scalar form
       const f32x2 bx = {__uint_as_float(s.z), __uint_as_float(s.w)};
@@ -1378,11 +1371,6 @@ __device__ bool obvh_walk(const TraceParams& P, uint32_t ob, d3 o, d3 d, double 
       const f32x2 bz = {__uint_as_float(s2.z), __uint_as_float(s2.w)};
       const f32x2 tx2 = (bx - ox2) * ix2, ty2 = (by - oy2) * iy2, tz2 = (bz - oz2) * iz2;
       const float tnx = tx2.x, tfx = tx2.y, tny = ty2.x, tfy = ty2.y, tnz = tz2.x, tfz = tz2.y;
-#else
-      const float tnx = (__uint_as_float(s.z) - ox) * ix, tfx = (__uint_as_float(s.w) - ox) * ix;
-      const float tny = (__uint_as_float(s2.x) - oy) * iy, tfy = (__uint_as_float(s2.y) - oy) * iy;
-      const float tnz = (__uint_as_float(s2.z) - oz) * iz, tfz = (__uint_as_float(s2.w) - oz) * iz;
-#endif
       // fmaxf / fminf drop a NaN bound (o on the bound's plane with inv = +-inf): no constraint
       const float tn = fmaxf(fmaxf(tmin_f, tnx), fmaxf(tny, tnz));
       const float tf = fminf(fminf(close_f, tfx), fminf(tfy, tfz));
@@ -1476,18 +1464,12 @@ __device__ bool cbvh_walk_t(const TraceParams& P, uint4 hd, d3 o, d3 d, double t
   const uint32_t sstep = 4u * blockDim.x;
   auto slot = [&](uint32_t off) { return reinterpret_cast<ls_t>(stack_b + off); };
   const d3 r = mk(rcp_nr1(d.x), rcp_nr1(d.y), rcp_nr1(d.z));
-#ifdef RT_OLD_INV  // A/B: the slab reciprocals from their own rcp + two Newton steps
-  const d3 inv = mk(rcp_w(d.x), rcp_w(d.y), rcp_w(d.z));
-  const bool nx = inv.x < 0.0, ny = inv.y < 0.0, nz = inv.z < 0.0;
-  const float ix = (float)inv.x, iy = (float)inv.y, iz = (float)inv.z;
-#else
   // The f32 slab reciprocals from the leaves' f64 ones (rcp_nr1, within an ulp of 1/d, then
   // rounded to f32 like 1/d itself: inside the box test's 2^-18 budget). d_a = +-0 gives NaN
   // there (rcp_nr1's 0 * inf), and a NaN slab time constrains nothing: every box is kept on
   // that axis, never dropped. The octant is d's sign bit (-0: the d_a < 0 side, as 1/-0 = -inf).
   const bool nx = __builtin_signbit(d.x), ny = __builtin_signbit(d.y), nz = __builtin_signbit(d.z);
   const float ix = (float)r.x, iy = (float)r.y, iz = (float)r.z;
-#endif
   constexpr float kBoxRel = 0x1p-20f;
   constexpr float kBoxPos = 1.0f + 0x1p-18f;
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
@@ -1727,20 +1709,11 @@ __device__ bool bvh_subtree(const TraceParams& P, uint32_t node, uint32_t stop, 
 // v_cvt_i32_f64 / v_cvt_u32_f64 compute; C++ leaves out-of-range conversions undefined, so the
 // instructions are issued directly (the compiler made each range check a branch; C4 -1.4 %,
 // profiles/r06i_ab_noise_c4.log; tests/test_gpu_parity.py::test_saturating_texture_coordinates)
-#ifdef RT_F2I_BRANCH  // A/B only: the range checks in C++
-__device__ __forceinline__ int32_t f2i_sat(double f) {
-  if (f != f) return 0;
-  if (f >= 2147483648.0) return 2147483647;
-  if (f <= -2147483648.0) return -2147483647 - 1;
-  return (int32_t)f;
-}
-#else
 __device__ __forceinline__ int32_t f2i_sat(double f) {
   int32_t r;
   asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(f));
   return r;
 }
-#endif
 __device__ __forceinline__ uint32_t f2u_sat(double f) {
   uint32_t r;
   asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(f));

@@ -28,24 +28,6 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) 
 // camera-ray block that seeds runs in nearly every bounce iteration of a wave.
 __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel,
                                         uint32_t sample) {
-#ifdef RT_SEED_PCG4D  // A/B only: round 5's key (a different stream; the oracle follows the default)
-  uint32_t v0 = pixel * 1664525u + 1013904223u, v1 = sample * 1664525u + 1013904223u;
-  uint32_t v2 = seed_lo * 1664525u + 1013904223u, v3 = seed_hi * 1664525u + 1013904223u;
-  v0 += v1 * v3;
-  v1 += v2 * v0;
-  v2 += v0 * v1;
-  v3 += v1 * v2;
-  v0 ^= v0 >> 16;
-  v1 ^= v1 >> 16;
-  v2 ^= v2 >> 16;
-  v3 ^= v3 >> 16;
-  v0 += v1 * v3;
-  v1 += v2 * v0;
-  v2 += v0 * v1;
-  v3 += v1 * v2;
-  v0 ^= v2;
-  v1 ^= v3;
-#else
   const uint32_t k0 = (seed_lo ^ 0x85EBCA6Bu) * 0x9E3779B9u + 1013904223u;
   const uint32_t k1 = (seed_hi ^ 0xC2B2AE35u) * 0x9E3779B9u + (k0 ^ 0x27D4EB2Fu);
   uint32_t v0 = pixel * 1664525u + k0, v1 = sample * 1664525u + k1;
@@ -57,23 +39,17 @@ __device__ __forceinline__ Rng rng_seed(uint32_t seed_lo, uint32_t seed_hi, uint
   v1 += v0 * 1664525u;
   v0 ^= v0 >> 16;
   v1 ^= v1 >> 16;
-#endif
   if ((v0 | v1) == 0u) v0 = 0x9E3779B9u;  // xoroshiro64*'s state must not be all zero
   return {v0, v1};
 }
 // xoroshiro64* (Blackman and Vigna): 32-bit outputs from 64 bits of state. The * scrambler (one
 // multiply) is the authors' generator for floating-point draws: its weak lowest bits land below
 // 2^-24 of a draw (random_double) or are discarded (random_int, a multiply-high). Round 5 used the
-// ** scrambler (a rotate and a second multiply on top); RT_RNG_STARSTAR restores it for A/B only
-// (a different stream: the oracle follows the default).
+// ** scrambler (a rotate and a second multiply on top; profiles/r06g_ab_rngstar_c{2,3,4}.log).
 __device__ __forceinline__ uint32_t rng_step(Rng& g) {
   const uint32_t s0 = g.s0;
   uint32_t s1 = g.s1;
-#ifdef RT_RNG_STARSTAR
-  const uint32_t result = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
-#else
   const uint32_t result = s0 * 0x9E3779BBu;
-#endif
   s1 ^= s0;
   g.s0 = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
   g.s1 = rotl32(s1, 13);
