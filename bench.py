@@ -373,6 +373,8 @@ def main():
                 "width": W, "height": H, "spp_effective": spp, "max_depth": cam.max_depth,
                 "seed": args.seed, "parallelism": f"cyclic rows x{world}, gather to rank 0",
                 "walker": walker,
+                "precision": "rays, hits and every path decision f64 (the reference's); radiance "
+                             "weights f32, sums f64 (DESIGN.md §2)",
             },
             "gather": gather_name,
         }
