@@ -2528,8 +2528,24 @@ __device__ __forceinline__ void trace_body(const TraceParams& P) {
     if (diel ? !tir : have_lights) u0 = rnd(g);
     const double r0s = front ? ldd(M, 5) : ldd(M, 6);  // Schlick r0 of `ratio` (host-derived)
     // reflectance r0 + (1 - r0) * (1 - cos)^5 in the reference's operation order (material.rs:
-    // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr)
-    const bool refl = tir || r0s + (1.0 - r0s) * pow5_cr(1.0 - cos_t) > u0;
+    // 156-163: a product, then a sum), with the power correctly rounded (pow5_cr). The test
+    // against u0 is decided from x^5 by three products (within 4.5 ulps of the correctly rounded
+    // power, so the reflectance is within 6.5 ulps of the exact one) unless u0 lies within 32
+    // ulps of it (a window of ~4e-15 relative, so about one draw in 10^14); those lanes take
+    // pow5_cr, and the decision is the exact one everywhere. (Kernels without a BVH only: C2
+    // -0.61 %, while the BVH kernel measured +0.51 %; profiles/r06l_ab_schlick_c{2,4}.log.)
+    const double sx = 1.0 - cos_t, omr = 1.0 - r0s;
+    bool refl_u;
+    if constexpr (!BVH) {
+      const double sx2 = sx * sx;
+      const double refl_f = r0s + omr * ((sx2 * sx2) * sx);
+      refl_u = refl_f > u0;
+      const bool near_u = fabs(refl_f - u0) <= refl_f * 0x1p-48;
+      if (__ballot(near_u) != 0ull && near_u) refl_u = r0s + omr * pow5_cr(sx) > u0;
+    } else {
+      refl_u = r0s + omr * pow5_cr(sx) > u0;
+    }
+    const bool refl = tir || refl_u;
     const bool light_branch = !diel && have_lights && u0 < 0.5;
     d3 dir;     // set on both arms below
     w3 factor;
