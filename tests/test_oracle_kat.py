@@ -47,6 +47,40 @@ def test_rng_deterministic_uniform_and_keyed():
     assert abs(c) < 0.05
 
 
+def _rng_restated(seed, pixel, sample, n):
+    """pcg2d key with seed-keyed increments, then xoroshiro64* (csrc/rt_rng.h rng_seed / rng_step,
+    DESIGN.md §4.1 RNG), restated in Python integers."""
+    m = 0xFFFFFFFF
+    lo, hi = seed & m, (seed >> 32) & m
+    k0 = (((lo ^ 0x85EBCA6B) * 0x9E3779B9) + 1013904223) & m
+    k1 = (((hi ^ 0xC2B2AE35) * 0x9E3779B9) + (k0 ^ 0x27D4EB2F)) & m
+    v0, v1 = (pixel * 1664525 + k0) & m, (sample * 1664525 + k1) & m
+    for _ in range(2):
+        v0 = (v0 + v1 * 1664525) & m
+        v1 = (v1 + v0 * 1664525) & m
+        v0 ^= v0 >> 16
+        v1 ^= v1 >> 16
+    if v0 | v1 == 0:
+        v0 = 0x9E3779B9
+    rotl = lambda x, k: ((x << k) | (x >> (32 - k))) & m  # noqa: E731
+    out = []
+    for _ in range(n):
+        out.append((v0 * 0x9E3779BB) & m)
+        s1 = v1 ^ v0
+        v0 = rotl(v0, 26) ^ s1 ^ ((s1 << 9) & m)
+        v1 = rotl(s1, 13)
+    return np.array(out, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(1, 0, 0), (1, 123, 45), (7, 639999, 960),
+                                               ((5 << 32) | 3, 2**31 + 7, 9999)])
+def test_rng_is_the_documented_generator(seed, pixel, sample):
+    """The oracle's stream is exactly pcg2d + xoroshiro64* (round 6, S4), so the device's
+    generator (the GPU tests require equal images) is the documented one too."""
+    got = O.rng_u32(seed, pixel, sample, 16).astype(np.uint64)
+    assert np.array_equal(got, _rng_restated(seed, pixel, sample, 16))
+
+
 # ---------------------------------------------------------------- camera (render.rs:218-249)
 def test_camera_ray_stratified_jitter():
     cam = rt.camera_new(1.0, 600, 1000, 50, 40.0, (278, 278, -800), (278, 278, 0), (0, 1, 0),
