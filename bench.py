@@ -149,7 +149,8 @@ def self_launch(n: int, argv) -> int:
     MASTER_ADDR / MASTER_PORT set as torchrun would, relay rank 0's stdout (its JSON line) and
     return non-zero if any rank fails. The parent never imports torch nor touches the GPU, and
     it starts children (no exec), so this is safe on the GPU box. A rank that fails ends the
-    others (they would wait in a barrier forever): exact child PIDs, SIGTERM then SIGKILL."""
+    others (they would wait in a barrier forever): exact child PIDs, SIGTERM then SIGKILL; a
+    SIGTERM / SIGINT / SIGHUP to the launcher is forwarded to the ranks the same way."""
     import socket
     import subprocess
     import threading
@@ -171,6 +172,22 @@ def self_launch(n: int, argv) -> int:
             sys.stdout.write(line.decode(errors="replace"))
             sys.stdout.flush()
 
+    import signal
+
+    def forward(signum, _frame):  # a launcher stopped by its caller stops its ranks first
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        deadline = time.time() + 20
+        while time.time() < deadline and any(p.poll() is None for p in procs):
+            time.sleep(0.2)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
     t.start()
     failed = None
@@ -212,6 +229,8 @@ def launch_check(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if os.environ.get("RT_LAUNCH_CHECK_FAIL_RANK") == str(rank):
         raise SystemExit(3)  # the launcher's failure path: the other ranks wait in rendezvous
+    if os.environ.get("RT_LAUNCH_CHECK_HOLD") == "1":
+        time.sleep(120)  # the launcher's signal path: ranks still running when it is stopped
     dist.init_process_group("gloo")
     dist.barrier()
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)

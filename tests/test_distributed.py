@@ -203,3 +203,35 @@ def test_bench_self_launch_fails_when_a_rank_fails():
     # WORLD_SIZE set (torchrun's contract) but != --gpus: refused, no self-launch
     r = _run_bench(["--gpus", "2", "--launch-check"], env_extra={"WORLD_SIZE": "3"}, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_self_launch_forwards_sigterm_to_its_ranks():
+    """Stopping the launcher (SIGTERM, as a driver's timeout does) stops its ranks too: no rank is
+    left running on a GPU. The ranks here hold before their rendezvous (RT_LAUNCH_CHECK_HOLD)."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+
+    import psutil
+
+    repo = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["RT_LAUNCH_CHECK_HOLD"] = "1"
+    p = subprocess.Popen([sys.executable, str(repo / "bench.py"), "--gpus", "3", "--launch-check"],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    kids = []
+    for _ in range(100):
+        kids = [c.pid for c in psutil.Process(p.pid).children()]
+        if len(kids) == 3:
+            break
+        time.sleep(0.1)
+    assert len(kids) == 3, kids
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    assert p.returncode == 128 + signal.SIGTERM, p.returncode
+    time.sleep(0.5)
+    assert not [k for k in kids if psutil.pid_exists(k) and
+                psutil.Process(k).status() != psutil.STATUS_ZOMBIE], kids
